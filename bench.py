@@ -1,0 +1,267 @@
+"""DCVC-DC encode+decode throughput on MI355X (BASELINE.json metric, config C3:
+DCVC-DC RGB 1920x1080, padded to 1088, IP=32, write mode = real bitstreams).
+
+One step = one frame through ``encode_decode(..., output_path=...)``: the
+I-frame codec when frame_idx % gop == 0, else the P-frame codec, exactly the
+loop of DCVC-DC/test_video.py:108-167.  Frames are synthetic (moving sinusoid
+pattern + noise, uint8, resident in HBM before timing); weights are seeded
+random in the reference's architecture (no checkpoints offline).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+
+Multi-GPU: one process per GPU (torchrun), each rank codes its own sequence
+(seed 1 + rank; the reference shards (sequence, rate) jobs the same way,
+test_video.py:396-436), weights are created on rank 0 and broadcast once over
+RCCL; no collective touches the per-frame path.  value = frames of all ranks
+/ max-over-ranks wall time.
+"""
+import argparse
+import json
+import os
+import time
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+PEAK_BF16_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
+PEAK_F32_TFLOPS = 157.3
+PEAK_HBM_GBS = 8000.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=32)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--gop", type=int, default=32)
+    ap.add_argument("--q_index", type=int, default=0)
+    ap.add_argument("--precision", choices=["fast", "parity"], default="fast")
+    ap.add_argument("--stream_part", type=int, default=1)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-roofline", action="store_true")
+    return ap.parse_args()
+
+
+def spec():
+    with open(os.path.join(HERE, "dcvc_amd", "data", "dc_param_spec.json")) as f:
+        d = json.load(f)
+    return [(n, tuple(s)) for n, s in d["intra"]], [(n, tuple(s)) for n, s in d["inter"]]
+
+
+def make_weights(dist, rank, device):
+    """Rank 0 builds the state dicts; one RCCL broadcast of the flat blob."""
+    from dcvc_amd.weights import synthetic_state_dict
+    i_spec, p_spec = spec()
+    names = [("i", n, s) for n, s in i_spec] + [("p", n, s) for n, s in p_spec]
+    total = sum(int(np.prod(s)) for _, _, s in names)
+    if rank == 0:
+        isd, psd = synthetic_state_dict(i_spec, seed=0), synthetic_state_dict(p_spec, seed=1)
+        flat = torch.cat([(isd if k == "i" else psd)[n].reshape(-1) for k, n, _ in names]).to(device)
+    else:
+        flat = torch.empty(total, dtype=torch.float32, device=device)
+    if dist is not None:
+        dist.broadcast(flat, 0)
+    flat = flat.cpu()
+    isd, psd, o = {}, {}, 0
+    for k, n, s in names:
+        m = int(np.prod(s))
+        (isd if k == "i" else psd)[n] = flat[o:o + m].reshape(s)
+        o += m
+    return isd, psd
+
+
+def cpu_baseline(isd, psd, args):
+    """Oracle (PyTorch fp32 CPU restatement, pinned to the reference) on a
+    bounded sample: one I-frame (untimed) then one P-frame encode+decode in
+    write mode at a quarter of the 1088x1920 area; fps scaled by area."""
+    from oracle import dc_oracle as O
+    from oracle import rans_oracle as R
+    from dcvc_amd.synth import moving_pattern, to_float
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    h, w = 544, 960
+    inet = O.IntraOracle(isd, R.pmf_to_quantized_cdf)
+    pnet = O.DMCOracle(psd, R.pmf_to_quantized_cdf)
+    tabs = {"i_y": (inet.y_cdf, inet.y_sizes, inet.y_offsets), "i_z": inet.z_tab,
+            "p_y": (pnet.y_cdf, pnet.y_sizes, pnet.y_offsets), "p_z": pnet.z_tab, "p_mvz": pnet.mvz_tab}
+
+    def code(calls, pre):
+        cc = [(s.clamp(-30000, 30000).to(torch.int16).numpy(), i.to(torch.int16).numpy(), tabs[pre + k])
+              for k, s, i in calls]
+        enc = R.DCStream()
+        st = enc.encode(cc)
+        dec = enc.decode(st)
+        pos = [0]
+
+        def decoder(kind, idx):
+            n = idx.numel()
+            v = dec[pos[0]:pos[0] + n]
+            pos[0] += n
+            return v
+        return decoder
+
+    frames = [torch.from_numpy(to_float(moving_pattern(h, w, t, seed=1))).unsqueeze(0) for t in range(2)]
+    with torch.no_grad():
+        t0 = time.time()
+        dec = code(inet.compress(frames[0], False, args.q_index), "i_")
+        xh = inet.decompress(dec, h, w, False, args.q_index)
+        t_i = time.time() - t0
+        dpb = {"ref_frame": xh, "ref_feature": None, "ref_mv_feature": None, "ref_y": None, "ref_mv_y": None}
+        t0 = time.time()
+        dec = code(pnet.compress(frames[1], dpb, False, args.q_index, 1), "p_")
+        pnet.decompress(dpb, dec, h, w, False, args.q_index, 1)
+        t_p = time.time() - t0
+    area = (1088 * 1920) / (h * w)
+    gop = args.gop
+    fps = gop / (area * (t_i + (gop - 1) * t_p))
+    return {"value": fps, "unit": "frames/s", "cores": threads, "kind": "port",
+            "sample": f"oracle write-mode I+P encode+decode at {h}x{w} (I {t_i:.1f}s, P {t_p:.1f}s), "
+                      f"scaled x{area:.1f} by area to 1088x1920, GOP {gop} average"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    device = torch.device("cuda", local)
+    torch.cuda.set_device(device)
+
+    from dcvc_amd import hip as K
+    from dcvc_amd.dc import DMC, IntraNoAR
+    from dcvc_amd.layers import Precision
+    from dcvc_amd.synth import moving_pattern
+
+    isd, psd = make_weights(dist, rank, device)
+    prec = Precision.fast() if args.precision == "fast" else Precision.parity()
+    inet = IntraNoAR(precision=prec, stream_part=args.stream_part, device=device).load_state_dict(isd)
+    pnet = DMC(precision=prec, stream_part=args.stream_part, device=device).load_state_dict(psd)
+    inet.update(force=True)
+    pnet.update(force=True)
+
+    h, w = args.height, args.width
+    H, W = (h + 15) // 16 * 16, (w + 15) // 16 * 16
+    nframes = args.warmup + args.steps
+    frames = [torch.from_numpy(moving_pattern(h, w, t, seed=1 + rank)).to(device) for t in range(nframes)]
+    out_dir = f"/dev/shm/dcvc_bench_{os.getpid()}"
+    os.makedirs(out_dir, exist_ok=True)
+    x = K.empty(H, W, 3, K.F32, device)
+    state = {"dpb": None}
+    bits = []
+    kinds = []
+
+    def step(i):
+        K.frame_to_nhwc(frames[i], h, w, x)     # uint8 CHW -> padded NHWC (replicate), test_video.py:130
+        path = os.path.join(out_dir, f"{i}.bin")
+        if i % args.gop == 0:
+            r = inet.encode_decode(x, False, args.q_index, path, pic_width=w, pic_height=h)
+            state["dpb"] = {"ref_frame": r["x_hat"], "ref_feature": None, "ref_mv_feature": None,
+                            "ref_y": None, "ref_mv_y": None}
+            kinds.append("I")
+        else:
+            r = pnet.encode_decode(x, state["dpb"], False, args.q_index, path, pic_width=w, pic_height=h,
+                                   frame_idx=i % 4)
+            state["dpb"] = r["dpb"]
+            kinds.append("P")
+        bits.append(r["bit"])
+
+    for i in range(args.warmup):
+        step(i)
+    torch.cuda.synchronize(device)
+    if dist is not None:
+        dist.barrier()
+    t0 = time.time()
+    per = []
+    for i in range(args.warmup, nframes):
+        ts = time.time()
+        step(i)
+        per.append(time.time() - ts)
+    torch.cuda.synchronize(device)
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.time() - t0
+    if dist is not None:
+        t = torch.tensor([elapsed], device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+
+    # ---- roofline of the dominant kernel family, from per-launch HIP events
+    # recorded on the stream the kernels run on, over one extra P-frame
+    roof = None
+    if not args.no_roofline and rank == 0:
+        K.PROFILE = []
+        step(nframes - 1 if (nframes - 1) % args.gop else nframes - 2)
+        torch.cuda.synchronize(device)
+        fam = {}
+        for f, e0, e1, fl, nb in K.PROFILE:
+            d = fam.setdefault(f, [0.0, 0, 0, 0])
+            d[0] += e0.elapsed_time(e1) * 1e-3
+            d[1] += fl
+            d[2] += nb
+            d[3] += 1
+        K.PROFILE = None
+        dom = max(fam, key=lambda k: fam[k][0])
+        tsec, fl, nb, n = fam[dom]
+        if dom == "conv":
+            ach = fl / tsec / 1e12
+            peak = PEAK_BF16_TFLOPS if args.precision == "fast" else PEAK_F32_TFLOPS
+            roof = {"bound": "mfma", "achieved": round(ach, 3), "peak": peak, "unit": "TFLOP/s",
+                    "frac": round(ach / peak, 5), "traffic": None}
+        else:
+            ach = nb / tsec / 1e9
+            roof = {"bound": "hbm", "achieved": round(ach, 2), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                    "frac": round(ach / PEAK_HBM_GBS, 5), "traffic": None}
+        roof["kernel"] = dom
+        roof["launches"] = n
+        roof["avg_launch_us"] = round(tsec / n * 1e6, 2)
+        roof["families_ms_per_P_frame"] = {k: round(v[0] * 1e3, 3) for k, v in fam.items()}
+
+    if rank == 0:
+        n_i = kinds[args.warmup:].count("I")
+        ti = [p for p, k in zip(per, kinds[args.warmup:]) if k == "I"]
+        tp = [p for p, k in zip(per, kinds[args.warmup:]) if k == "P"]
+        cpu = None
+        if not args.no_cpu_baseline and world == 1:
+            cpu = cpu_baseline(isd, psd, args)
+        timed_bits = bits[args.warmup:nframes]
+        line = {
+            "metric": "encode+decode fps @1080p per GPU (DCVC-DC write mode, real bitstreams)",
+            "value": round(world * args.steps / elapsed, 4),
+            "unit": "frames/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16" if args.precision == "fast" else "f32",
+            "data": "synthetic (moving sinusoid + noise frames, seeded random weights)",
+            "config": {"workload": f"C3 DCVC-DC RGB {w}x{h} (pad {W}x{H}) IP={args.gop} write mode",
+                       "gop": args.gop, "q_index": args.q_index, "precision": args.precision,
+                       "stream_part": args.stream_part, "parallelism": f"sequence-sharded x{world}",
+                       "I_frames_timed": n_i,
+                       "ms_I": round(1e3 * float(np.mean(ti)), 2) if ti else None,
+                       "ms_P": round(1e3 * float(np.mean(tp)), 2) if tp else None,
+                       "bpp": round(float(np.mean(timed_bits)) / (h * w), 5)},
+            "roofline": roof,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    for f in os.listdir(out_dir):
+        os.remove(os.path.join(out_dir, f))
+    os.rmdir(out_dir)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

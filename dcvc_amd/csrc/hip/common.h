@@ -1,0 +1,57 @@
+// Shared device helpers for the gfx950 kernels of libdcvc_hip.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <hip/hip_bf16.h>
+#include <stdint.h>
+
+#include "../../../include/dcvc_hip.h"
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef uint16_t u16x4 __attribute__((ext_vector_type(4)));
+typedef uint16_t u16x8 __attribute__((ext_vector_type(8)));
+
+// bf16 is carried as raw uint16 in memory; conversion is round-to-nearest-even
+// (v_cvt_pk_bf16_f32 on gfx950).
+__device__ __forceinline__ float bf2f(uint16_t v) {
+  return __uint_as_float(((uint32_t)v) << 16);
+}
+__device__ __forceinline__ uint16_t f2bf(float f) {
+  __hip_bfloat16 b = __float2bfloat16(f);
+  return *reinterpret_cast<uint16_t *>(&b);
+}
+
+template <typename T> struct Elem;
+template <> struct Elem<float> {
+  __device__ __forceinline__ static float load(const float *p) { return *p; }
+  __device__ __forceinline__ static void store(float *p, float v) { *p = v; }
+};
+template <> struct Elem<uint16_t> {
+  __device__ __forceinline__ static float load(const uint16_t *p) { return bf2f(*p); }
+  __device__ __forceinline__ static void store(uint16_t *p, float v) { *p = f2bf(v); }
+};
+
+template <typename T>
+__device__ __forceinline__ float ld(const void *base, int64_t i) {
+  return Elem<T>::load(reinterpret_cast<const T *>(base) + i);
+}
+template <typename T>
+__device__ __forceinline__ void st(void *base, int64_t i, float v) {
+  Elem<T>::store(reinterpret_cast<T *>(base) + i, v);
+}
+
+// Epilogue / prologue activations (see dcvc_act in dcvc_hip.h).
+__device__ __forceinline__ float apply_act(int act, float v, float slope) {
+  switch (act) {
+    case DCVC_ACT_LRELU: return v >= 0.f ? v : v * slope;
+    case DCVC_ACT_CLAMP01: return fminf(fmaxf(v, 0.f), 1.f);
+    case DCVC_ACT_ROUND: return rintf(v);
+    default: return v;
+  }
+}
+
+#define DCVC_LAUNCH_CHECK()                          \
+  do {                                               \
+    hipError_t e__ = hipGetLastError();              \
+    if (e__ != hipSuccess) return DCVC_HIP_ELAUNCH;  \
+  } while (0)

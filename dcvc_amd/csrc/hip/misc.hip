@@ -1,0 +1,355 @@
+// Depthwise conv, elementwise/copy/pad kernels and the quadtree-prior
+// quantise / index / dequantise kernels.
+#include "common.h"
+
+namespace {
+
+struct View {
+  void *p;
+  int H, W, C, cs, co;
+};
+View mk(const dcvc_tensor &t) { return View{t.ptr, t.H, t.W, t.C, t.cstride, t.coff}; }
+
+bool ok(const dcvc_tensor &t) {
+  return t.ptr && t.H > 0 && t.W > 0 && t.C > 0 && t.coff >= 0 && t.coff + t.C <= t.cstride &&
+         (t.dtype == DCVC_F32 || t.dtype == DCVC_BF16);
+}
+
+#define DISPATCH2(tx, ty, KERNEL)                                        \
+  do {                                                                   \
+    if ((tx) == DCVC_F32 && (ty) == DCVC_F32) { KERNEL(float, float); }  \
+    else if ((tx) == DCVC_F32) { KERNEL(float, uint16_t); }              \
+    else if ((ty) == DCVC_F32) { KERNEL(uint16_t, float); }              \
+    else { KERNEL(uint16_t, uint16_t); }                                 \
+  } while (0)
+
+inline unsigned blocks_for(int64_t n, int bs = 256) { return (unsigned)((n + bs - 1) / bs); }
+
+// ------------------------------------------------------------ depthwise 3x3
+template <typename TX, typename TY>
+__global__ void dw_kernel(View x, View y, const float *w, const float *b) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (int64_t)y.H * y.W * y.C) return;
+  const int c = (int)(idx % y.C);
+  const int64_t pix = idx / y.C;
+  const int py = (int)(pix / y.W), px = (int)(pix - (int64_t)py * y.W);
+  float acc = 0.f;
+#pragma unroll
+  for (int dy = -1; dy <= 1; ++dy) {
+    const int yy = py + dy;
+    if (yy < 0 || yy >= x.H) continue;
+#pragma unroll
+    for (int dx = -1; dx <= 1; ++dx) {
+      const int xx = px + dx;
+      if (xx < 0 || xx >= x.W) continue;
+      acc += w[((dy + 1) * 3 + dx + 1) * y.C + c] * ld<TX>(x.p, ((int64_t)yy * x.W + xx) * x.cs + x.co + c);
+    }
+  }
+  st<TY>(y.p, pix * y.cs + y.co + c, acc + b[c]);
+}
+
+// ------------------------------------------------------------ elementwise
+template <typename TA, typename TY>
+__global__ void add_kernel(View a, View b, int b32, View y) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (int64_t)y.H * y.W * y.C) return;
+  const int c = (int)(idx % y.C);
+  const int64_t pix = idx / y.C;
+  const float va = ld<TA>(a.p, pix * a.cs + a.co + c);
+  const float vb = b32 ? ld<float>(b.p, pix * b.cs + b.co + c) : ld<uint16_t>(b.p, pix * b.cs + b.co + c);
+  st<TY>(y.p, pix * y.cs + y.co + c, va + vb);
+}
+
+template <typename TX, typename TY>
+__global__ void copy_kernel(View x, View y) {
+  // replicate-pad / crop / dtype convert: y(py, px) = x(min(py, H-1), min(px, W-1))
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (int64_t)y.H * y.W * y.C) return;
+  const int c = (int)(idx % y.C);
+  const int64_t pix = idx / y.C;
+  const int py = (int)(pix / y.W), px = (int)(pix - (int64_t)py * y.W);
+  const int sy = min(py, x.H - 1), sx = min(px, x.W - 1);
+  st<TY>(y.p, pix * y.cs + y.co + c, ld<TX>(x.p, ((int64_t)sy * x.W + sx) * x.cs + x.co + c));
+}
+
+template <typename TY>
+__global__ void frame_kernel(const uint8_t *src, int h, int w, View y) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (int64_t)y.H * y.W * 3) return;
+  const int c = (int)(idx % 3);
+  const int64_t pix = idx / 3;
+  const int py = (int)(pix / y.W), px = (int)(pix - (int64_t)py * y.W);
+  const int sy = min(py, h - 1), sx = min(px, w - 1);
+  const float v = (float)src[((int64_t)c * h + sy) * w + sx] / 255.f;
+  st<TY>(y.p, pix * y.cs + y.co + c, v);
+}
+
+// ------------------------------------------------------------ quadtree prior
+// Step k processes, for each pixel with parity m = 2*(y&1) + (x&1), the
+// channel quarter q with STEP_MASK[k][q] == m (common_model.py:168-220).
+__constant__ int kStepMask[4][4] = {{0, 1, 2, 3}, {3, 2, 1, 0}, {2, 3, 0, 1}, {1, 0, 3, 2}};
+
+__device__ __forceinline__ int quarter_of(int k, int m) {
+  int q = 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    if (kStepMask[k][i] == m) q = i;
+  return q;
+}
+
+__device__ __forceinline__ int16_t scale_index(float s, float log_min, float log_step) {
+  // GaussianEncoder.build_indexes (entropy_models.py:269-273)
+  s = fmaxf(s, 1e-5f);
+  float v = (logf(s) - log_min) / log_step;
+  v = fminf(fmaxf(v, 0.f), 255.f);
+  return (int16_t)(int)v;
+}
+
+struct QT {
+  View y, params, sm, yhs, yhat;
+  int has_sm;
+  int C;  // latent channels
+};
+
+__device__ __forceinline__ void step_scales_means(const QT &t, int64_t pix, int q, int cc, float &sc,
+                                                  float &me) {
+  const int C4 = t.C / 4;
+  if (t.has_sm) {
+    sc = ld<float>(t.sm.p, pix * t.sm.cs + t.sm.co + q * C4 + cc);
+    me = ld<float>(t.sm.p, pix * t.sm.cs + t.sm.co + t.C + q * C4 + cc);
+  } else {
+    sc = ld<float>(t.params.p, pix * t.params.cs + t.params.co + t.C + q * C4 + cc);
+    me = ld<float>(t.params.p, pix * t.params.cs + t.params.co + 2 * t.C + q * C4 + cc);
+  }
+}
+
+// one thread per (channel-in-quarter cc, pixel): NCHW order of y_q_w_k
+__global__ void qt_encode_kernel(QT t, int k, int16_t *sym, int16_t *idx, float log_min,
+                                 float log_step) {
+  const int C4 = t.C / 4;
+  const int64_t HW = (int64_t)t.y.H * t.y.W;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= HW * C4) return;
+  const int cc = (int)(i / HW);
+  const int64_t pix = i - (int64_t)cc * HW;
+  const int py = (int)(pix / t.y.W), px = (int)(pix - (int64_t)py * t.y.W);
+  const int m = ((py & 1) << 1) | (px & 1);
+  const int q = quarter_of(k, m);
+  const int ch = q * C4 + cc;
+  float qs = ld<float>(t.params.p, pix * t.params.cs + t.params.co + ch);
+  qs = fmaxf(qs, 0.5f);                                  // clamp_min(quant_step, 0.5)
+  const float yv = ld<float>(t.y.p, pix * t.y.cs + t.y.co + ch) / qs;
+  float sc, me;
+  step_scales_means(t, pix, q, cc, sc, me);
+  const float yres = yv - me;                            // (y - means*1) * 1
+  const float yq = rintf(yres);
+  const float yh = yq + me;
+  const float cl = fminf(fmaxf(yq, -30000.f), 30000.f);
+  sym[i] = (int16_t)(int)cl;
+  idx[i] = scale_index(sc, log_min, log_step);
+  st<float>(t.yhs.p, pix * t.yhs.cs + t.yhs.co + ch, yh);
+  st<float>(t.yhat.p, pix * t.yhat.cs + t.yhat.co + ch, yh * qs);
+}
+
+__global__ void qt_index_kernel(QT t, int k, int16_t *idx, float log_min, float log_step) {
+  const int C4 = t.C / 4;
+  const int64_t HW = (int64_t)t.params.H * t.params.W;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= HW * C4) return;
+  const int cc = (int)(i / HW);
+  const int64_t pix = i - (int64_t)cc * HW;
+  const int py = (int)(pix / t.params.W), px = (int)(pix - (int64_t)py * t.params.W);
+  const int q = quarter_of(k, ((py & 1) << 1) | (px & 1));
+  float sc, me;
+  step_scales_means(t, pix, q, cc, sc, me);
+  idx[i] = scale_index(sc, log_min, log_step);
+}
+
+__global__ void qt_decode_kernel(QT t, int k, const int16_t *sym) {
+  const int C4 = t.C / 4;
+  const int64_t HW = (int64_t)t.params.H * t.params.W;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= HW * C4) return;
+  const int cc = (int)(i / HW);
+  const int64_t pix = i - (int64_t)cc * HW;
+  const int py = (int)(pix / t.params.W), px = (int)(pix - (int64_t)py * t.params.W);
+  const int q = quarter_of(k, ((py & 1) << 1) | (px & 1));
+  const int ch = q * C4 + cc;
+  float sc, me;
+  step_scales_means(t, pix, q, cc, sc, me);
+  float qs = ld<float>(t.params.p, pix * t.params.cs + t.params.co + ch);
+  qs = fmaxf(qs, 0.5f);
+  const float yh = ((float)sym[i] + me);                 // (y_q_r + means) * 1
+  st<float>(t.yhs.p, pix * t.yhs.cs + t.yhs.co + ch, yh);
+  st<float>(t.yhat.p, pix * t.yhat.cs + t.yhat.co + ch, yh * qs);
+}
+
+template <typename TX>
+__global__ void to_sym_kernel(View x, int16_t *sym) {
+  const int64_t HW = (int64_t)x.H * x.W;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= HW * x.C) return;
+  const int c = (int)(i / HW);
+  const int64_t pix = i - (int64_t)c * HW;
+  const float v = fminf(fmaxf(ld<TX>(x.p, pix * x.cs + x.co + c), -30000.f), 30000.f);
+  sym[i] = (int16_t)(int)v;
+}
+
+template <typename TY>
+__global__ void from_sym_kernel(const int16_t *sym, View y) {
+  const int64_t HW = (int64_t)y.H * y.W;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= HW * y.C) return;
+  const int c = (int)(i / HW);
+  const int64_t pix = i - (int64_t)c * HW;
+  st<TY>(y.p, pix * y.cs + y.co + c, (float)sym[i]);
+}
+
+bool qt_ok(const dcvc_tensor &params, const dcvc_tensor &sm, int C) {
+  if (!ok(params) || params.dtype != DCVC_F32 || params.C != 3 * C || (C % 4)) return false;
+  if (sm.ptr && (!ok(sm) || sm.dtype != DCVC_F32 || sm.C != 2 * C || sm.H != params.H || sm.W != params.W))
+    return false;
+  return true;
+}
+
+}  // namespace
+
+extern "C" int dcvc_dwconv3x3(dcvc_tensor x, dcvc_tensor y, const float *w, const float *bias,
+                              void *stream) {
+  if (!ok(x) || !ok(y) || !w || !bias || x.C != y.C || x.H != y.H || x.W != y.W) return DCVC_HIP_EINVAL;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const unsigned g = blocks_for((int64_t)y.H * y.W * y.C);
+#define K(TX, TY) hipLaunchKernelGGL((dw_kernel<TX, TY>), dim3(g), dim3(256), 0, st, mk(x), mk(y), w, bias)
+  DISPATCH2(x.dtype, y.dtype, K);
+#undef K
+  DCVC_LAUNCH_CHECK();
+  return DCVC_HIP_OK;
+}
+
+extern "C" int dcvc_add(dcvc_tensor a, dcvc_tensor b, dcvc_tensor y, void *stream) {
+  if (!ok(a) || !ok(b) || !ok(y) || a.C != y.C || b.C != y.C || a.H != y.H || b.H != y.H ||
+      a.W != y.W || b.W != y.W)
+    return DCVC_HIP_EINVAL;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const unsigned g = blocks_for((int64_t)y.H * y.W * y.C);
+  const int b32 = b.dtype == DCVC_F32;
+#define K(TX, TY) hipLaunchKernelGGL((add_kernel<TX, TY>), dim3(g), dim3(256), 0, st, mk(a), mk(b), b32, mk(y))
+  DISPATCH2(a.dtype, y.dtype, K);
+#undef K
+  DCVC_LAUNCH_CHECK();
+  return DCVC_HIP_OK;
+}
+
+static int copy_impl(dcvc_tensor x, dcvc_tensor y, void *stream) {
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const unsigned g = blocks_for((int64_t)y.H * y.W * y.C);
+#define K(TX, TY) hipLaunchKernelGGL((copy_kernel<TX, TY>), dim3(g), dim3(256), 0, st, mk(x), mk(y))
+  DISPATCH2(x.dtype, y.dtype, K);
+#undef K
+  DCVC_LAUNCH_CHECK();
+  return DCVC_HIP_OK;
+}
+
+extern "C" int dcvc_copy(dcvc_tensor x, dcvc_tensor y, void *stream) {
+  if (!ok(x) || !ok(y) || x.C != y.C || x.H != y.H || x.W != y.W) return DCVC_HIP_EINVAL;
+  return copy_impl(x, y, stream);
+}
+
+extern "C" int dcvc_pad_replicate(dcvc_tensor x, dcvc_tensor y, void *stream) {
+  if (!ok(x) || !ok(y) || x.C != y.C) return DCVC_HIP_EINVAL;
+  return copy_impl(x, y, stream);
+}
+
+extern "C" int dcvc_frame_to_nhwc(const uint8_t *src, int h, int w, dcvc_tensor y, void *stream) {
+  if (!src || !ok(y) || y.C != 3 || h <= 0 || w <= 0 || y.H < h || y.W < w) return DCVC_HIP_EINVAL;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const unsigned g = blocks_for((int64_t)y.H * y.W * 3);
+  if (y.dtype == DCVC_F32)
+    hipLaunchKernelGGL((frame_kernel<float>), dim3(g), dim3(256), 0, st, src, h, w, mk(y));
+  else
+    hipLaunchKernelGGL((frame_kernel<uint16_t>), dim3(g), dim3(256), 0, st, src, h, w, mk(y));
+  DCVC_LAUNCH_CHECK();
+  return DCVC_HIP_OK;
+}
+
+extern "C" int dcvc_quadtree_encode_step(dcvc_tensor y, dcvc_tensor params, dcvc_tensor sm, int k,
+                                         dcvc_tensor yhs, dcvc_tensor yhat, int16_t *symbols,
+                                         int16_t *indexes, float log_min, float log_step,
+                                         void *stream) {
+  const int C = y.C;
+  if (!ok(y) || y.dtype != DCVC_F32 || !qt_ok(params, sm, C) || k < 0 || k > 3) return DCVC_HIP_EINVAL;
+  if ((k == 0) != (sm.ptr == nullptr)) return DCVC_HIP_EINVAL;
+  if (!ok(yhs) || !ok(yhat) || yhs.dtype != DCVC_F32 || yhat.dtype != DCVC_F32 || yhs.C != C ||
+      yhat.C != C || !symbols || !indexes)
+    return DCVC_HIP_EINVAL;
+  if (params.H != y.H || params.W != y.W || yhs.H != y.H || yhat.H != y.H || yhs.W != y.W || yhat.W != y.W)
+    return DCVC_HIP_EINVAL;
+  QT t{mk(y), mk(params), mk(sm), mk(yhs), mk(yhat), sm.ptr != nullptr, C};
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const unsigned g = blocks_for((int64_t)y.H * y.W * (C / 4));
+  hipLaunchKernelGGL(qt_encode_kernel, dim3(g), dim3(256), 0, st, t, k, symbols, indexes, log_min, log_step);
+  DCVC_LAUNCH_CHECK();
+  return DCVC_HIP_OK;
+}
+
+extern "C" int dcvc_quadtree_indexes_step(dcvc_tensor params, dcvc_tensor sm, int k, int16_t *indexes,
+                                          float log_min, float log_step, void *stream) {
+  const int C = params.C / 3;
+  if (!qt_ok(params, sm, C) || k < 0 || k > 3 || !indexes) return DCVC_HIP_EINVAL;
+  if ((k == 0) != (sm.ptr == nullptr)) return DCVC_HIP_EINVAL;
+  QT t{};
+  t.params = mk(params);
+  t.sm = mk(sm);
+  t.has_sm = sm.ptr != nullptr;
+  t.C = C;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const unsigned g = blocks_for((int64_t)params.H * params.W * (C / 4));
+  hipLaunchKernelGGL(qt_index_kernel, dim3(g), dim3(256), 0, st, t, k, indexes, log_min, log_step);
+  DCVC_LAUNCH_CHECK();
+  return DCVC_HIP_OK;
+}
+
+extern "C" int dcvc_quadtree_decode_step(dcvc_tensor params, dcvc_tensor sm, int k, const int16_t *symbols,
+                                         dcvc_tensor yhs, dcvc_tensor yhat, void *stream) {
+  const int C = params.C / 3;
+  if (!qt_ok(params, sm, C) || k < 0 || k > 3 || !symbols) return DCVC_HIP_EINVAL;
+  if ((k == 0) != (sm.ptr == nullptr)) return DCVC_HIP_EINVAL;
+  if (!ok(yhs) || !ok(yhat) || yhs.dtype != DCVC_F32 || yhat.dtype != DCVC_F32 || yhs.C != C || yhat.C != C)
+    return DCVC_HIP_EINVAL;
+  QT t{};
+  t.params = mk(params);
+  t.sm = mk(sm);
+  t.yhs = mk(yhs);
+  t.yhat = mk(yhat);
+  t.has_sm = sm.ptr != nullptr;
+  t.C = C;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const unsigned g = blocks_for((int64_t)params.H * params.W * (C / 4));
+  hipLaunchKernelGGL(qt_decode_kernel, dim3(g), dim3(256), 0, st, t, k, symbols);
+  DCVC_LAUNCH_CHECK();
+  return DCVC_HIP_OK;
+}
+
+extern "C" int dcvc_nhwc_to_symbols(dcvc_tensor x, int16_t *symbols, void *stream) {
+  if (!ok(x) || !symbols) return DCVC_HIP_EINVAL;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const unsigned g = blocks_for((int64_t)x.H * x.W * x.C);
+  if (x.dtype == DCVC_F32)
+    hipLaunchKernelGGL((to_sym_kernel<float>), dim3(g), dim3(256), 0, st, mk(x), symbols);
+  else
+    hipLaunchKernelGGL((to_sym_kernel<uint16_t>), dim3(g), dim3(256), 0, st, mk(x), symbols);
+  DCVC_LAUNCH_CHECK();
+  return DCVC_HIP_OK;
+}
+
+extern "C" int dcvc_symbols_to_nhwc(const int16_t *symbols, dcvc_tensor y, void *stream) {
+  if (!ok(y) || !symbols) return DCVC_HIP_EINVAL;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const unsigned g = blocks_for((int64_t)y.H * y.W * y.C);
+  if (y.dtype == DCVC_F32)
+    hipLaunchKernelGGL((from_sym_kernel<float>), dim3(g), dim3(256), 0, st, symbols, mk(y));
+  else
+    hipLaunchKernelGGL((from_sym_kernel<uint16_t>), dim3(g), dim3(256), 0, st, symbols, mk(y));
+  DCVC_LAUNCH_CHECK();
+  return DCVC_HIP_OK;
+}

@@ -1,0 +1,277 @@
+// Gather / resampling kernels: bilinear flow warp (grid_sample border,
+// align_corners=True), the fused OffsetDiversity warp+fusion, bilinear x2
+// resize (align_corners=False) and 2x2 pooling.
+//
+// The float arithmetic follows the PyTorch CPU kernels the reference runs on
+// (unnormalize as (g + 1) * ((size - 1) / 2), clip, floor-based bilinear
+// weights, corner sum nw + ne + sw + se; separable resize as
+// (x00*w0 + x01*w1)*h0 + (x10*w0 + x11*w1)*h1; avg pool as a running sum / 4)
+// with FMA contraction disabled, so the f32 path can match the CPU oracle
+// element for element.
+#include "common.h"
+
+#pragma clang fp contract(off)
+
+namespace {
+
+struct View {
+  void *p;
+  int H, W, C, cs, co;
+};
+View mk(const dcvc_tensor &t) { return View{t.ptr, t.H, t.W, t.C, t.cstride, t.coff}; }
+
+bool ok(const dcvc_tensor &t) {
+  return t.ptr && t.H > 0 && t.W > 0 && t.C > 0 && t.coff >= 0 && t.coff + t.C <= t.cstride &&
+         (t.dtype == DCVC_F32 || t.dtype == DCVC_BF16);
+}
+
+struct Bilin {
+  int x0, x1, y0, y1;
+  float nw, ne, sw, se;
+};
+
+// grid_sample(bilinear, border, align_corners=True) sample position for
+// pixel (x, y) displaced by (fx, fy) pixels (video_net.py:22-33).
+__device__ __forceinline__ Bilin warp_coords(float gxv, float gyv, float fx, float fy, int W, int H) {
+  const float fxn = fx / (float)((W - 1.0) / 2.0);
+  const float fyn = fy / (float)((H - 1.0) / 2.0);
+  const float grid_x = gxv + fxn;
+  const float grid_y = gyv + fyn;
+  float ix = (grid_x + 1.f) * ((float)(W - 1) / 2.f);
+  float iy = (grid_y + 1.f) * ((float)(H - 1) / 2.f);
+  ix = fminf((float)(W - 1), fmaxf(ix, 0.f));
+  iy = fminf((float)(H - 1), fmaxf(iy, 0.f));
+  const float xw = floorf(ix), yn = floorf(iy);
+  const float w = ix - xw, e = 1.f - w, n = iy - yn, s = 1.f - n;
+  Bilin b;
+  b.x0 = (int)xw;
+  b.y0 = (int)yn;
+  b.x1 = min(b.x0 + 1, W - 1);
+  b.y1 = min(b.y0 + 1, H - 1);
+  b.nw = s * e;
+  b.ne = s * w;
+  b.sw = n * e;
+  b.se = n * w;
+  return b;
+}
+
+template <typename T>
+__device__ __forceinline__ float sample(const View &x, const Bilin &b, int c) {
+  const int64_t r0 = (int64_t)b.y0 * x.W, r1 = (int64_t)b.y1 * x.W;
+  const float vnw = ld<T>(x.p, (r0 + b.x0) * x.cs + x.co + c);
+  const float vne = ld<T>(x.p, (r0 + b.x1) * x.cs + x.co + c);
+  const float vsw = ld<T>(x.p, (r1 + b.x0) * x.cs + x.co + c);
+  const float vse = ld<T>(x.p, (r1 + b.x1) * x.cs + x.co + c);
+  return vnw * b.nw + vne * b.ne + vsw * b.sw + vse * b.se;
+}
+
+template <typename TX, typename TY>
+__global__ void warp_kernel(View x, View f, View y, const float *gx, const float *gy) {
+  const int64_t pix = (int64_t)blockIdx.x * blockDim.y + threadIdx.y;
+  if (pix >= (int64_t)y.H * y.W) return;
+  const int py = (int)(pix / y.W), px = (int)(pix - (int64_t)py * y.W);
+  const float fx = ld<float>(f.p, pix * f.cs + f.co);
+  const float fy = ld<float>(f.p, pix * f.cs + f.co + 1);
+  const Bilin b = warp_coords(gx[px], gy[py], fx, fy, x.W, x.H);
+  for (int c = threadIdx.x; c < y.C; c += blockDim.x)
+    st<TY>(y.p, pix * y.cs + y.co + c, sample<TX>(x, b, c));
+}
+
+// bilinear x2 upsample value of channel c at full-res pixel (oy, ox) from a
+// half-res map (align_corners=False, UpSampleKernel.cpp cpu_upsample_linear)
+template <typename T>
+__device__ __forceinline__ float up2_at(const View &m, int oy, int ox, int c) {
+  float sy = 0.5f * ((float)oy + 0.5f) - 0.5f;
+  float sx = 0.5f * ((float)ox + 0.5f) - 0.5f;
+  sy = sy < 0.f ? 0.f : sy;
+  sx = sx < 0.f ? 0.f : sx;
+  const int h0 = (int)sy, w0 = (int)sx;
+  const int h1 = h0 + (h0 < m.H - 1 ? 1 : 0), w1 = w0 + (w0 < m.W - 1 ? 1 : 0);
+  const float hl1 = sy - (float)h0, hl0 = 1.f - hl1;
+  const float wl1 = sx - (float)w0, wl0 = 1.f - wl1;
+  const float a = ld<T>(m.p, ((int64_t)h0 * m.W + w0) * m.cs + m.co + c);
+  const float b = ld<T>(m.p, ((int64_t)h0 * m.W + w1) * m.cs + m.co + c);
+  const float cc = ld<T>(m.p, ((int64_t)h1 * m.W + w0) * m.cs + m.co + c);
+  const float d = ld<T>(m.p, ((int64_t)h1 * m.W + w1) * m.cs + m.co + c);
+  return (a * wl0 + b * wl1) * hl0 + (cc * wl0 + d * wl1) * hl1;
+}
+
+__device__ __forceinline__ float sigmoidf_(float v) { return 1.f / (1.f + expf(-v)); }
+
+// OffsetDiversity (video_model.py:43-63), one thread per (pixel, group g):
+// warps i = 2g, 2g+1 feed fusion group g (output channels 3g..3g+2).
+template <typename TF, typename TO, typename TY>
+__global__ void offset_div_kernel(View feat, View offs, View flow, View y, const float *fw,
+                                  const float *fb, const float *gx, const float *gy, float mag) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int g = (int)(t & 15);
+  const int64_t pix = t >> 4;
+  if (pix >= (int64_t)y.H * y.W) return;
+  const int py = (int)(pix / y.W), px = (int)(pix - (int64_t)py * y.W);
+  const float fx = ld<float>(flow.p, pix * flow.cs + flow.co);
+  const float fy = ld<float>(flow.p, pix * flow.cs + flow.co + 1);
+  float xm[6];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int i = 2 * g + k;                       // warp index 0..31
+    // offset channels 2i, 2i+1 of cat(o1, o2) = channels 2i, 2i+1 of the map
+    float dx = mag * tanhf(up2_at<TO>(offs, py, px, 2 * i));
+    float dy = mag * tanhf(up2_at<TO>(offs, py, px, 2 * i + 1));
+    dx = dx + fx;                                  // flow.repeat: even ch -> dx
+    dy = dy + fy;
+    const float msk = sigmoidf_(up2_at<TO>(offs, py, px, 64 + i));
+    const Bilin b = warp_coords(gx[px], gy[py], dx, dy, feat.W, feat.H);
+    const int src_group = i & 15;                  // x.repeat(2,1,1,1)
+#pragma unroll
+    for (int c = 0; c < 3; ++c) xm[3 * k + c] = sample<TF>(feat, b, 3 * src_group + c) * msk;
+  }
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    const int o = 3 * g + c;
+    float acc = 0.f;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) acc = acc + fw[o * 6 + k] * xm[k];
+    st<TY>(y.p, pix * y.cs + y.co + o, acc + fb[o]);
+  }
+}
+
+template <typename TX, typename TY>
+__global__ void resize_kernel(View x, View y, int up, float mul) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t total = (int64_t)y.H * y.W * y.C;
+  if (idx >= total) return;
+  const int c = (int)(idx % y.C);
+  const int64_t pix = idx / y.C;
+  const int oy = (int)(pix / y.W), ox = (int)(pix - (int64_t)oy * y.W);
+  float v;
+  if (up) {
+    v = up2_at<TX>(x, oy, ox, c);
+  } else {
+    const float scy = (float)x.H / (float)y.H, scx = (float)x.W / (float)y.W;
+    float sy = scy * ((float)oy + 0.5f) - 0.5f;
+    float sx = scx * ((float)ox + 0.5f) - 0.5f;
+    sy = sy < 0.f ? 0.f : sy;
+    sx = sx < 0.f ? 0.f : sx;
+    const int h0 = (int)sy, w0 = (int)sx;
+    const int h1 = h0 + (h0 < x.H - 1 ? 1 : 0), w1 = w0 + (w0 < x.W - 1 ? 1 : 0);
+    const float hl1 = sy - (float)h0, hl0 = 1.f - hl1;
+    const float wl1 = sx - (float)w0, wl0 = 1.f - wl1;
+    const float a = ld<TX>(x.p, ((int64_t)h0 * x.W + w0) * x.cs + x.co + c);
+    const float b = ld<TX>(x.p, ((int64_t)h0 * x.W + w1) * x.cs + x.co + c);
+    const float cc = ld<TX>(x.p, ((int64_t)h1 * x.W + w0) * x.cs + x.co + c);
+    const float d = ld<TX>(x.p, ((int64_t)h1 * x.W + w1) * x.cs + x.co + c);
+    v = (a * wl0 + b * wl1) * hl0 + (cc * wl0 + d * wl1) * hl1;
+  }
+  st<TY>(y.p, pix * y.cs + y.co + c, v * mul);
+}
+
+template <typename TX, typename TY>
+__global__ void pool_kernel(View x, View y, int is_max) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t total = (int64_t)y.H * y.W * y.C;
+  if (idx >= total) return;
+  const int c = (int)(idx % y.C);
+  const int64_t pix = idx / y.C;
+  const int oy = (int)(pix / y.W), ox = (int)(pix - (int64_t)oy * y.W);
+  const int64_t r0 = (int64_t)(2 * oy) * x.W, r1 = r0 + x.W;
+  const float a = ld<TX>(x.p, (r0 + 2 * ox) * x.cs + x.co + c);
+  const float b = ld<TX>(x.p, (r0 + 2 * ox + 1) * x.cs + x.co + c);
+  const float cc = ld<TX>(x.p, (r1 + 2 * ox) * x.cs + x.co + c);
+  const float d = ld<TX>(x.p, (r1 + 2 * ox + 1) * x.cs + x.co + c);
+  float v;
+  if (is_max) {
+    v = a;
+    v = (b > v || isnan(b)) ? b : v;
+    v = (cc > v || isnan(cc)) ? cc : v;
+    v = (d > v || isnan(d)) ? d : v;
+  } else {
+    float s = 0.f;
+    s = s + a;
+    s = s + b;
+    s = s + cc;
+    s = s + d;
+    v = s / 4.f;
+  }
+  st<TY>(y.p, pix * y.cs + y.co + c, v);
+}
+
+#define DISPATCH2(tx, ty, KERNEL, ...)                                         \
+  do {                                                                         \
+    if ((tx) == DCVC_F32 && (ty) == DCVC_F32) { KERNEL(float, float, __VA_ARGS__); }            \
+    else if ((tx) == DCVC_F32) { KERNEL(float, uint16_t, __VA_ARGS__); }                        \
+    else if ((ty) == DCVC_F32) { KERNEL(uint16_t, float, __VA_ARGS__); }                        \
+    else { KERNEL(uint16_t, uint16_t, __VA_ARGS__); }                                           \
+  } while (0)
+
+}  // namespace
+
+extern "C" int dcvc_flow_warp(dcvc_tensor x, dcvc_tensor flow, dcvc_tensor y, const float *gx,
+                              const float *gy, void *stream) {
+  if (!ok(x) || !ok(flow) || !ok(y) || !gx || !gy) return DCVC_HIP_EINVAL;
+  if (flow.dtype != DCVC_F32 || flow.C != 2 || flow.H != y.H || flow.W != y.W || x.H != y.H ||
+      x.W != y.W || x.C != y.C)
+    return DCVC_HIP_EINVAL;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int tpc = y.C >= 32 ? 32 : (y.C >= 8 ? 8 : 4);  // threads per pixel
+  const int ppb = 256 / tpc;
+  const int64_t npix = (int64_t)y.H * y.W;
+  dim3 blk(tpc, ppb);
+  dim3 grd((unsigned)((npix + ppb - 1) / ppb));
+#define K(TX, TY, ...) hipLaunchKernelGGL((warp_kernel<TX, TY>), grd, blk, 0, st, mk(x), mk(flow), mk(y), gx, gy)
+  DISPATCH2(x.dtype, y.dtype, K, 0);
+#undef K
+  DCVC_LAUNCH_CHECK();
+  return DCVC_HIP_OK;
+}
+
+extern "C" int dcvc_offset_diversity(dcvc_tensor feat, dcvc_tensor offs, dcvc_tensor flow,
+                                     dcvc_tensor y, const float *fw, const float *fb,
+                                     const float *gx, const float *gy, float max_mag,
+                                     void *stream) {
+  if (!ok(feat) || !ok(offs) || !ok(flow) || !ok(y) || !fw || !fb || !gx || !gy)
+    return DCVC_HIP_EINVAL;
+  if (feat.C != 48 || y.C != 48 || offs.C != 96 || flow.C != 2 || flow.dtype != DCVC_F32 ||
+      feat.H != y.H || feat.W != y.W || flow.H != y.H || flow.W != y.W ||
+      offs.H * 2 != y.H || offs.W * 2 != y.W)
+    return DCVC_HIP_EINVAL;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int64_t threads = (int64_t)y.H * y.W * 16;
+  const unsigned grd = (unsigned)((threads + 255) / 256);
+#define LAUNCH(TF, TO, TY)                                                                  \
+  hipLaunchKernelGGL((offset_div_kernel<TF, TO, TY>), dim3(grd), dim3(256), 0, st, mk(feat), \
+                     mk(offs), mk(flow), mk(y), fw, fb, gx, gy, max_mag)
+  const bool f32 = feat.dtype == DCVC_F32, o32 = offs.dtype == DCVC_F32, y32 = y.dtype == DCVC_F32;
+  if (f32 && o32 && y32) LAUNCH(float, float, float);
+  else if (!f32 && !o32 && !y32) LAUNCH(uint16_t, uint16_t, uint16_t);
+  else if (!f32 && o32 && !y32) LAUNCH(uint16_t, float, uint16_t);
+  else return DCVC_HIP_EUNSUPPORTED;
+#undef LAUNCH
+  DCVC_LAUNCH_CHECK();
+  return DCVC_HIP_OK;
+}
+
+extern "C" int dcvc_resize2x(dcvc_tensor x, dcvc_tensor y, int up, float mul, void *stream) {
+  if (!ok(x) || !ok(y) || x.C != y.C) return DCVC_HIP_EINVAL;
+  if (up ? (y.H != 2 * x.H || y.W != 2 * x.W) : (y.H != x.H / 2 || y.W != x.W / 2))
+    return DCVC_HIP_EINVAL;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int64_t total = (int64_t)y.H * y.W * y.C;
+  const unsigned grd = (unsigned)((total + 255) / 256);
+#define K(TX, TY, ...) hipLaunchKernelGGL((resize_kernel<TX, TY>), dim3(grd), dim3(256), 0, st, mk(x), mk(y), up, mul)
+  DISPATCH2(x.dtype, y.dtype, K, 0);
+#undef K
+  DCVC_LAUNCH_CHECK();
+  return DCVC_HIP_OK;
+}
+
+extern "C" int dcvc_pool2x2(dcvc_tensor x, dcvc_tensor y, int is_max, void *stream) {
+  if (!ok(x) || !ok(y) || x.C != y.C || y.H != x.H / 2 || y.W != x.W / 2) return DCVC_HIP_EINVAL;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int64_t total = (int64_t)y.H * y.W * y.C;
+  const unsigned grd = (unsigned)((total + 255) / 256);
+#define K(TX, TY, ...) hipLaunchKernelGGL((pool_kernel<TX, TY>), dim3(grd), dim3(256), 0, st, mk(x), mk(y), is_max)
+  DISPATCH2(x.dtype, y.dtype, K, 0);
+#undef K
+  DCVC_LAUNCH_CHECK();
+  return DCVC_HIP_OK;
+}

@@ -1,0 +1,140 @@
+"""Shared pieces of the DC codecs: the quadtree (four-part) prior driver and
+per-frame symbol staging (DCVC-DC/src/models/common_model.py:13-321)."""
+import numpy as np
+import torch
+
+from .. import hip as K
+from ..hip import F32
+from ..layers import DepthConvBlock, cast
+from ..stream_helper import get_padding_size
+
+
+class SymbolBuffer:
+    """Device int16 staging for one frame's coder calls: every call's
+    symbols (and indexes) land in one device buffer that is copied to pinned
+    host memory with a single transfer."""
+
+    def __init__(self, device):
+        self.dev = device
+        self.sizes = []
+        self.kinds = []
+
+    def plan(self, kind, n):
+        self.kinds.append(kind)
+        self.sizes.append(n)
+        return len(self.sizes) - 1
+
+    def alloc(self):
+        total = int(sum(self.sizes))
+        self.sym = torch.empty(total, dtype=torch.int16, device=self.dev)
+        self.idx = torch.empty(total, dtype=torch.int16, device=self.dev)
+        self.offs = np.concatenate([[0], np.cumsum(self.sizes)]).astype(np.int64)
+        return self
+
+    def sym_slice(self, i):
+        return self.sym[self.offs[i]:self.offs[i + 1]]
+
+    def idx_slice(self, i):
+        return self.idx[self.offs[i]:self.offs[i + 1]]
+
+    def to_host(self):
+        s = torch.empty(self.sym.numel(), dtype=torch.int16, pin_memory=True)
+        x = torch.empty(self.idx.numel(), dtype=torch.int16, pin_memory=True)
+        s.copy_(self.sym, non_blocking=True)
+        x.copy_(self.idx, non_blocking=True)
+        torch.cuda.current_stream().synchronize()
+        s, x = s.numpy(), x.numpy()
+        return [(s[self.offs[i]:self.offs[i + 1]], x[self.offs[i]:self.offs[i + 1]]) for i in range(len(self.sizes))]
+
+
+class QuadtreePrior:
+    """forward/compress/decompress_four_part_prior (common_model.py:142-321).
+
+    The spatial-prior input cat(y_hat_so_far, common_params) is one fp32
+    NHWC buffer of 4C channels: the prior fusion writes common_params into
+    channels [C, 4C) and the quantise kernels write y_hat_so_far into [0, C).
+    """
+
+    def __init__(self, ctx, adaptor_names, spatial_prefix, C, gated, nblocks=3):
+        self.C = C
+        self.adaptors = [ctx.conv(n, latent=True) for n in adaptor_names]
+        self.spatial = [DepthConvBlock(ctx, f"{spatial_prefix}.{i}", gated=gated, latent=True)
+                        for i in range(nblocks)]
+        self.ctx = ctx
+
+    def new_buffer(self, h, w):
+        buf = K.empty(h, w, 4 * self.C, F32, self.ctx.dev)
+        buf.buf[:, :, :self.C].zero_()
+        return buf
+
+    def step_params(self, buf, k):
+        x = K.conv(self.adaptors[k - 1], buf)
+        for b in self.spatial:
+            x = b(x)
+        return x  # 2C: scales_0..3 | means_0..3
+
+    def encode(self, y, buf, symbuf, calls, scale_table):
+        C = self.C
+        yhat = K.empty(y.H, y.W, C, F32, self.ctx.dev)
+        params = buf.ch(C, 3 * C)
+        for k in range(4):
+            sm = None if k == 0 else self.step_params(buf, k)
+            K.qt_encode_step(y, params, sm, k, buf.ch(0, C), yhat, symbuf.sym_slice(calls[k]),
+                             symbuf.idx_slice(calls[k]), scale_table.log_min, scale_table.log_step)
+        return yhat
+
+    def decode(self, buf, decode_fn, scale_table):
+        """decode_fn(host int16 indexes) -> host int16 symbols."""
+        C = self.C
+        h, w = buf.H, buf.W
+        n = h * w * (C // 4)
+        dev = self.ctx.dev
+        yhat = K.empty(h, w, C, F32, dev)
+        params = buf.ch(C, 3 * C)
+        idx_d = torch.empty(n, dtype=torch.int16, device=dev)
+        idx_h = torch.empty(n, dtype=torch.int16, pin_memory=True)
+        sym_h = torch.empty(n, dtype=torch.int16, pin_memory=True)
+        sym_d = torch.empty(n, dtype=torch.int16, device=dev)
+        for k in range(4):
+            sm = None if k == 0 else self.step_params(buf, k)
+            K.qt_indexes_step(params, sm, k, idx_d, scale_table.log_min, scale_table.log_step)
+            idx_h.copy_(idx_d, non_blocking=True)
+            torch.cuda.current_stream().synchronize()
+            sym_h.numpy()[:] = decode_fn(idx_h.numpy())
+            sym_d.copy_(sym_h, non_blocking=True)
+            K.qt_decode_step(params, sm, k, sym_d, buf.ch(0, C), yhat)
+        return yhat
+
+
+def pad_for_y(y):
+    """common_model.py:70-78: replicate-pad the latent to a multiple of 4."""
+    _, r, _, b = get_padding_size(y.H, y.W, 4)
+    if r == 0 and b == 0:
+        return y
+    out = K.empty(y.H + b, y.W + r, y.C, y.dtype, y.buf.device)
+    return K.pad_replicate(y, out)
+
+
+def crop_to(x, h, w, y=None):
+    """slice_to_y (common_model.py:85-86): top-left crop."""
+    if x.H == h and x.W == w and y is None:
+        return x
+    if y is None:
+        y = K.empty(h, w, x.C, x.dtype, x.buf.device)
+    return K.pad_replicate(x, y)
+
+
+def q_fine(q_scale):
+    """load_state_dict fine tables (video_model.py:325-341)."""
+    q = q_scale.detach().float().cpu()
+    return np.exp(np.linspace(np.log(q[0, 0, 0, 0]), np.log(q[3, 0, 0, 0]), 64))
+
+
+def curr_q(table, basic, q_index, device):
+    """get_curr_q (common_model.py:35-37) on the host CPU, uploaded as a
+    per-channel fp32 vector."""
+    q = basic.detach().float().cpu() * table[q_index]
+    return q.reshape(-1).contiguous().to(device)
+
+
+__all__ = ["SymbolBuffer", "QuadtreePrior", "pad_for_y", "crop_to", "q_fine", "curr_q", "cast"]

@@ -1,0 +1,302 @@
+"""ctypes bindings of libdcvc_hip (include/dcvc_hip.h) over PyTorch-ROCm memory.
+
+Activations are ``Act`` views: a torch tensor ``buf`` of shape (H, W, Cbuf)
+(NHWC, batch 1, on the GPU) plus a channel window (coff, C).  torch is only
+the allocator and the stream provider; every computation below is one of our
+kernels.  Calls are asynchronous on the current HIP stream.
+"""
+import ctypes
+
+import numpy as np
+import torch
+
+from ._native import hip_lib, check
+
+F32, BF16 = 0, 1
+ACT_NONE, ACT_LRELU, ACT_CLAMP01, ACT_ROUND = 0, 1, 2, 3
+IN_NONE, IN_LRELU, IN_GATE = 0, 1, 2
+
+_TORCH = {F32: torch.float32, BF16: torch.bfloat16}
+_CODE = {torch.float32: F32, torch.bfloat16: BF16}
+
+
+class CTensor(ctypes.Structure):
+    _fields_ = [("ptr", ctypes.c_void_p), ("dtype", ctypes.c_int), ("H", ctypes.c_int),
+                ("W", ctypes.c_int), ("C", ctypes.c_int), ("cstride", ctypes.c_int),
+                ("coff", ctypes.c_int)]
+
+
+class CConvArgs(ctypes.Structure):
+    _fields_ = [("x", CTensor), ("y", CTensor), ("w", ctypes.c_void_p), ("bias", ctypes.c_void_p),
+                ("cin", ctypes.c_int), ("cout", ctypes.c_int), ("kh", ctypes.c_int), ("kw", ctypes.c_int),
+                ("stride", ctypes.c_int), ("pad", ctypes.c_int), ("compute", ctypes.c_int),
+                ("in_op", ctypes.c_int), ("in_slope", ctypes.c_float), ("act", ctypes.c_int),
+                ("slope", ctypes.c_float), ("shuffle", ctypes.c_int), ("scale", ctypes.c_void_p),
+                ("res", CTensor), ("res2", CTensor)]
+
+
+_T = CTensor
+_vp, _i, _f = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
+HIP_SYMBOLS = [
+    ("dcvc_conv_pack_weights", ctypes.c_int64, [_vp, _i, _i, _i, _i, _i, _vp]),
+    ("dcvc_conv2d", _i, [ctypes.POINTER(CConvArgs), _vp]),
+    ("dcvc_dwconv3x3", _i, [_T, _T, _vp, _vp, _vp]),
+    ("dcvc_flow_warp", _i, [_T, _T, _T, _vp, _vp, _vp]),
+    ("dcvc_offset_diversity", _i, [_T, _T, _T, _T, _vp, _vp, _vp, _vp, _f, _vp]),
+    ("dcvc_resize2x", _i, [_T, _T, _i, _f, _vp]),
+    ("dcvc_pool2x2", _i, [_T, _T, _i, _vp]),
+    ("dcvc_add", _i, [_T, _T, _T, _vp]),
+    ("dcvc_copy", _i, [_T, _T, _vp]),
+    ("dcvc_pad_replicate", _i, [_T, _T, _vp]),
+    ("dcvc_frame_to_nhwc", _i, [_vp, _i, _i, _T, _vp]),
+    ("dcvc_quadtree_encode_step", _i, [_T, _T, _T, _i, _T, _T, _vp, _vp, _f, _f, _vp]),
+    ("dcvc_quadtree_indexes_step", _i, [_T, _T, _i, _vp, _f, _f, _vp]),
+    ("dcvc_quadtree_decode_step", _i, [_T, _T, _i, _vp, _T, _T, _vp]),
+    ("dcvc_nhwc_to_symbols", _i, [_T, _vp, _vp]),
+    ("dcvc_symbols_to_nhwc", _i, [_vp, _T, _vp]),
+]
+
+_L = None
+
+# Optional per-launch timing (bench.py roofline): when a list, each kernel
+# wrapper records (family, start event, end event, algorithmic flops, bytes).
+PROFILE = None
+
+
+def _t0():
+    if PROFILE is None:
+        return None
+    e = torch.cuda.Event(enable_timing=True)
+    e.record()
+    return e
+
+
+def _t1(e0, family, flops, nbytes):
+    if e0 is None:
+        return
+    e = torch.cuda.Event(enable_timing=True)
+    e.record()
+    PROFILE.append((family, e0, e, flops, nbytes))
+
+
+def _esz(dtype):
+    return 4 if dtype == F32 else 2
+
+
+def lib():
+    global _L
+    if _L is None:
+        _L = hip_lib()
+    return _L
+
+
+def stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+class Act:
+    """NHWC view: channels [coff, coff + C) of buf (H, W, Cbuf)."""
+    __slots__ = ("buf", "coff", "C")
+
+    def __init__(self, buf, coff=0, C=None):
+        assert buf.dim() == 3 and buf.is_contiguous()
+        self.buf = buf
+        self.coff = coff
+        self.C = buf.shape[2] - coff if C is None else C
+
+    @property
+    def H(self):
+        return self.buf.shape[0]
+
+    @property
+    def W(self):
+        return self.buf.shape[1]
+
+    @property
+    def dtype(self):
+        return _CODE[self.buf.dtype]
+
+    def ch(self, off, n):
+        assert 0 <= off and off + n <= self.C
+        return Act(self.buf, self.coff + off, n)
+
+    def c(self):
+        return CTensor(self.buf.data_ptr(), self.dtype, self.H, self.W, self.C, self.buf.shape[2], self.coff)
+
+    def t(self):
+        """torch view (H, W, C)."""
+        return self.buf[:, :, self.coff:self.coff + self.C]
+
+    def nchw(self):
+        return self.t().permute(2, 0, 1).unsqueeze(0).float()
+
+
+NULL_T = CTensor(None, 0, 0, 0, 0, 0, 0)
+
+
+def empty(H, W, C, dtype, device=None):
+    dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
+    return Act(torch.empty((H, W, C), dtype=_TORCH[dtype], device=dev))
+
+
+def zeros(H, W, C, dtype, device=None):
+    dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
+    return Act(torch.zeros((H, W, C), dtype=_TORCH[dtype], device=dev))
+
+
+def from_nchw(x, dtype=F32):
+    """(1, C, H, W) tensor -> Act (test / harness helper)."""
+    t = x[0].permute(1, 2, 0).contiguous().to(_TORCH[dtype])
+    if not t.is_cuda:
+        t = t.cuda()
+    return Act(t)
+
+
+class ConvW:
+    """A conv layer's packed weights.  Reference layout [Cout][Cin][kh][kw]
+    (nn.Conv2d state_dict), packed once to [Cout][kh][kw][Cin_pad32]."""
+
+    def __init__(self, weight, bias, stride=1, compute=BF16, device=None):
+        w = weight.detach().float().cpu().contiguous()
+        self.cout, self.cin, self.kh, self.kw = (int(s) for s in w.shape)
+        self.stride = stride
+        self.pad = (self.kh - 1) // 2
+        self.compute = compute
+        cinp = (self.cin + 31) // 32 * 32
+        n = self.cout * self.kh * self.kw * cinp
+        host = np.zeros(n, dtype=np.float32 if compute == F32 else np.uint16)
+        wn = w.numpy()
+        got = lib().dcvc_conv_pack_weights(wn.ctypes.data_as(ctypes.c_void_p), self.cout, self.cin,
+                                           self.kh, self.kw, compute, host.ctypes.data_as(ctypes.c_void_p))
+        check(int(got), "conv_pack_weights")
+        dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
+        if compute == F32:
+            self.w = torch.from_numpy(host).to(dev)
+        else:
+            self.w = torch.from_numpy(host.view(np.int16)).to(dev)
+        b = bias.detach().float().cpu() if bias is not None else torch.zeros(self.cout)
+        self.b = b.contiguous().to(dev)
+
+    def out_hw(self, H, W):
+        return (H + 2 * self.pad - self.kh) // self.stride + 1, (W + 2 * self.pad - self.kw) // self.stride + 1
+
+
+def conv(cw, x, y=None, *, out_dtype=None, in_op=IN_NONE, in_slope=0.0, act=ACT_NONE, slope=0.0,
+         shuffle=False, scale=None, res=None, res2=None):
+    """y = scale * (res2 + (res + act(conv(in_op(x)) + bias))), optional pixel shuffle."""
+    Ho, Wo = cw.out_hw(x.H, x.W)
+    cy = cw.cout // 4 if shuffle else cw.cout
+    if y is None:
+        f = 2 if shuffle else 1
+        y = empty(Ho * f, Wo * f, cy, out_dtype if out_dtype is not None else x.dtype, x.buf.device)
+    a = CConvArgs()
+    a.x = x.c()
+    a.y = y.c()
+    a.w = cw.w.data_ptr()
+    a.bias = cw.b.data_ptr()
+    a.cin, a.cout, a.kh, a.kw = cw.cin, cw.cout, cw.kh, cw.kw
+    a.stride, a.pad, a.compute = cw.stride, cw.pad, cw.compute
+    a.in_op, a.in_slope, a.act, a.slope = in_op, in_slope, act, slope
+    a.shuffle = 1 if shuffle else 0
+    a.scale = scale.data_ptr() if scale is not None else None
+    a.res = res.c() if res is not None else NULL_T
+    a.res2 = res2.c() if res2 is not None else NULL_T
+    e0 = _t0()
+    check(lib().dcvc_conv2d(ctypes.byref(a), stream()), "conv2d")
+    if e0 is not None:
+        flops = 2 * Ho * Wo * cw.cout * cw.cin * cw.kh * cw.kw
+        nb = (x.H * x.W * x.C * _esz(x.dtype) + cw.w.numel() * cw.w.element_size()
+              + y.H * y.W * y.C * _esz(y.dtype) * (1 + (res is not None) + (res2 is not None)))
+        _t1(e0, "conv", flops, nb)
+    return y
+
+
+def dwconv3x3(x, w9c, b, y=None):
+    if y is None:
+        y = empty(x.H, x.W, x.C, x.dtype, x.buf.device)
+    e0 = _t0()
+    check(lib().dcvc_dwconv3x3(x.c(), y.c(), w9c.data_ptr(), b.data_ptr(), stream()), "dwconv3x3")
+    _t1(e0, "dwconv", 18 * x.H * x.W * x.C, x.H * x.W * x.C * (_esz(x.dtype) + _esz(y.dtype)))
+    return y
+
+
+def flow_warp(x, flow, grid, y=None):
+    if y is None:
+        y = empty(x.H, x.W, x.C, x.dtype, x.buf.device)
+    gx, gy = grid
+    e0 = _t0()
+    check(lib().dcvc_flow_warp(x.c(), flow.c(), y.c(), gx.data_ptr(), gy.data_ptr(), stream()), "flow_warp")
+    _t1(e0, "warp", 8 * y.H * y.W * y.C, y.H * y.W * (y.C * (_esz(x.dtype) + _esz(y.dtype)) + 8))
+    return y
+
+
+def offset_diversity(feat, offs_half, flow, fw, fb, grid, y=None, max_mag=40.0):
+    if y is None:
+        y = empty(feat.H, feat.W, 48, feat.dtype, feat.buf.device)
+    gx, gy = grid
+    e0 = _t0()
+    check(lib().dcvc_offset_diversity(feat.c(), offs_half.c(), flow.c(), y.c(), fw.data_ptr(), fb.data_ptr(),
+                                      gx.data_ptr(), gy.data_ptr(), max_mag, stream()), "offset_diversity")
+    _t1(e0, "offset_diversity", y.H * y.W * 48 * 20, y.H * y.W * (96 * _esz(feat.dtype) + 8))
+    return y
+
+
+def resize2x(x, up, mul=1.0, y=None, out_dtype=None):
+    if y is None:
+        H, W = (x.H * 2, x.W * 2) if up else (x.H // 2, x.W // 2)
+        y = empty(H, W, x.C, out_dtype if out_dtype is not None else x.dtype, x.buf.device)
+    check(lib().dcvc_resize2x(x.c(), y.c(), 1 if up else 0, mul, stream()), "resize2x")
+    return y
+
+
+def pool2x2(x, is_max, y=None):
+    if y is None:
+        y = empty(x.H // 2, x.W // 2, x.C, x.dtype, x.buf.device)
+    check(lib().dcvc_pool2x2(x.c(), y.c(), 1 if is_max else 0, stream()), "pool2x2")
+    return y
+
+
+def add(a, b, y=None):
+    if y is None:
+        y = empty(a.H, a.W, a.C, a.dtype, a.buf.device)
+    check(lib().dcvc_add(a.c(), b.c(), y.c(), stream()), "add")
+    return y
+
+
+def copy(x, y):
+    check(lib().dcvc_copy(x.c(), y.c(), stream()), "copy")
+    return y
+
+
+def pad_replicate(x, y):
+    check(lib().dcvc_pad_replicate(x.c(), y.c(), stream()), "pad_replicate")
+    return y
+
+
+def frame_to_nhwc(src_u8, h, w, y):
+    check(lib().dcvc_frame_to_nhwc(src_u8.data_ptr(), h, w, y.c(), stream()), "frame_to_nhwc")
+    return y
+
+
+def qt_encode_step(y, params, sm, k, yhs, yhat, sym, idx, log_min, log_step):
+    check(lib().dcvc_quadtree_encode_step(y.c(), params.c(), sm.c() if sm is not None else NULL_T, k,
+                                          yhs.c(), yhat.c(), sym.data_ptr(), idx.data_ptr(),
+                                          log_min, log_step, stream()), "quadtree_encode_step")
+
+
+def qt_indexes_step(params, sm, k, idx, log_min, log_step):
+    check(lib().dcvc_quadtree_indexes_step(params.c(), sm.c() if sm is not None else NULL_T, k,
+                                           idx.data_ptr(), log_min, log_step, stream()), "quadtree_indexes_step")
+
+
+def qt_decode_step(params, sm, k, sym, yhs, yhat):
+    check(lib().dcvc_quadtree_decode_step(params.c(), sm.c() if sm is not None else NULL_T, k,
+                                          sym.data_ptr(), yhs.c(), yhat.c(), stream()), "quadtree_decode_step")
+
+
+def to_symbols(x, sym):
+    check(lib().dcvc_nhwc_to_symbols(x.c(), sym.data_ptr(), stream()), "nhwc_to_symbols")
+
+
+def from_symbols(sym, y):
+    check(lib().dcvc_symbols_to_nhwc(sym.data_ptr(), y.c(), stream()), "symbols_to_nhwc")

@@ -1,0 +1,277 @@
+"""Network blocks of the DCVC-DC hot path on libdcvc_hip.
+
+Each block is built from a reference-format state_dict prefix (same key names
+as DCVC-DC/src/models/*.py, so reference checkpoints load) and runs entirely
+on our kernels: convs with fused epilogues, depthwise conv, pooling, resize.
+Concatenations are never materialised by copying: producers write into
+channel windows of one NHWC buffer (``Act.ch``).
+
+Precision policy (``Precision``): feature-domain activations (full to 1/8
+resolution) are stored in ``feat`` and convolved with ``feat_compute``;
+latent-domain tensors (1/16 and 1/64: y, z, priors, entropy parameters) are
+stored fp32 and convolved with ``latent_compute``.  ``Precision.parity()`` is
+fp32 everywhere (f32 MFMA, exact fp32 fma chains); ``Precision.fast()`` is
+bf16 MFMA with fp32 accumulation and fp32 latents.
+"""
+import torch
+
+from . import hip as K
+from .hip import Act, F32, BF16, ACT_LRELU, ACT_NONE, IN_LRELU, IN_GATE
+
+
+class Precision:
+    def __init__(self, feat, feat_compute, latent_compute):
+        self.feat = feat
+        self.feat_compute = feat_compute
+        self.latent = F32
+        self.latent_compute = latent_compute
+
+    @staticmethod
+    def parity():
+        return Precision(F32, F32, F32)
+
+    @staticmethod
+    def fast(latent_compute=F32):
+        return Precision(BF16, BF16, latent_compute)
+
+
+class Ctx:
+    """Builds layers from a state_dict on one device under one precision."""
+
+    def __init__(self, state_dict, device, prec):
+        self.sd = state_dict
+        self.dev = device
+        self.prec = prec
+
+    def has(self, name):
+        return name + ".weight" in self.sd
+
+    def conv(self, name, stride=1, latent=False, compute=None):
+        if compute is None:
+            compute = self.prec.latent_compute if latent else self.prec.feat_compute
+        return K.ConvW(self.sd[name + ".weight"], self.sd.get(name + ".bias"), stride, compute, self.dev)
+
+    def dw(self, name):
+        w = self.sd[name + ".weight"].detach().float().cpu()  # [C,1,3,3]
+        C = w.shape[0]
+        w9c = w.reshape(C, 9).t().contiguous().to(self.dev)  # [9][C]
+        b = self.sd[name + ".bias"].detach().float().contiguous().to(self.dev)
+        return w9c, b
+
+    def dtype(self, latent):
+        return self.prec.latent if latent else self.prec.feat
+
+    def fit(self, x, compute):
+        """f32 compute needs f32 inputs; cast a view when a layer crosses domains."""
+        if compute == F32 and x.dtype != F32:
+            return cast(x, F32)
+        return x
+
+
+def cast(x, dtype):
+    if x.dtype == dtype:
+        return x
+    y = K.empty(x.H, x.W, x.C, dtype, x.buf.device)
+    return K.copy(x, y)
+
+
+# ------------------------------------------------------------------ layers.py
+class DepthConvBlock:
+    """DepthConv + ConvFFN (DepthConvBlock) or + ConvFFN2 (DepthConvBlock2),
+    DCVC-DC/src/models/layers.py:135-222."""
+
+    def __init__(self, ctx, p, gated=False, latent=False, slope_dc=0.01, slope_ffn=0.1):
+        self.ctx, self.latent, self.gated = ctx, latent, gated
+        self.slope_dc, self.slope_ffn = slope_dc, slope_ffn
+        d = p + ".block.0"
+        f = p + ".block.1"
+        self.conv1 = ctx.conv(d + ".conv1.0", latent=latent)
+        self.dw = ctx.dw(d + ".depth_conv")
+        self.conv2 = ctx.conv(d + ".conv2", latent=latent)
+        self.adaptor = ctx.conv(d + ".adaptor", latent=latent) if ctx.has(d + ".adaptor") else None
+        if gated:
+            self.ffn1 = ctx.conv(f + ".conv", latent=latent)
+            self.ffn2 = ctx.conv(f + ".conv_out", latent=latent)
+        else:
+            self.ffn1 = ctx.conv(f + ".conv.0", latent=latent)
+            self.ffn2 = ctx.conv(f + ".conv.2", latent=latent)
+        self.cout = self.ffn2.cout
+
+    def __call__(self, x, y=None, scale=None):
+        ctx = self.ctx
+        dt = ctx.dtype(self.latent)
+        x = ctx.fit(x, self.conv1.compute)
+        if self.adaptor is not None:
+            idn = K.conv(self.adaptor, x, out_dtype=dt)
+        else:
+            idn = cast(x, dt)
+        t = K.conv(self.conv1, x, out_dtype=dt, act=ACT_LRELU, slope=self.slope_dc)
+        t = K.dwconv3x3(t, *self.dw)
+        dc = K.conv(self.conv2, t, res=idn)
+        if self.gated:
+            h = K.conv(self.ffn1, dc)
+            return K.conv(self.ffn2, h, y, in_op=IN_GATE, in_slope=self.slope_ffn, res=dc, scale=scale)
+        h = K.conv(self.ffn1, dc, act=ACT_LRELU, slope=self.slope_ffn)
+        return K.conv(self.ffn2, h, y, act=ACT_LRELU, slope=self.slope_ffn, res=dc, scale=scale)
+
+
+class ResidualBlockWithStride:
+    """layers.py:42-73."""
+
+    def __init__(self, ctx, p, latent=False):
+        self.ctx, self.latent = ctx, latent
+        self.conv1 = ctx.conv(p + ".conv1", 2, latent)
+        self.conv2 = ctx.conv(p + ".conv2", 1, latent)
+        self.down = ctx.conv(p + ".downsample", 2, latent)
+
+    def __call__(self, x, y=None, scale=None):
+        dt = self.ctx.dtype(self.latent)
+        x = self.ctx.fit(x, self.conv1.compute)
+        t = K.conv(self.conv1, x, out_dtype=dt, act=ACT_LRELU, slope=0.01)
+        idn = K.conv(self.down, x, out_dtype=dt)
+        return K.conv(self.conv2, t, y, act=ACT_LRELU, slope=0.1, res=idn, scale=scale)
+
+
+class ResidualBlockUpsample:
+    """layers.py:76-101."""
+
+    def __init__(self, ctx, p, latent=False):
+        self.ctx, self.latent = ctx, latent
+        self.sub = ctx.conv(p + ".subpel_conv.0", 1, latent)
+        self.conv = ctx.conv(p + ".conv", 1, latent)
+        self.up = ctx.conv(p + ".upsample.0", 1, latent)
+
+    def __call__(self, x, y=None, scale=None):
+        dt = self.ctx.dtype(self.latent)
+        x = self.ctx.fit(x, self.sub.compute)
+        t = K.conv(self.sub, x, out_dtype=dt, shuffle=True, act=ACT_LRELU, slope=0.01)
+        idn = K.conv(self.up, x, out_dtype=dt, shuffle=True)
+        return K.conv(self.conv, t, y, act=ACT_LRELU, slope=0.1, res=idn, scale=scale)
+
+
+# ------------------------------------------------------------ video_net.py
+class ResBlock:
+    """video_net.py:58-76: x + [lrelu?](conv2(lrelu(conv1(lrelu(x)))))."""
+
+    def __init__(self, ctx, p, slope=0.01, end_with_relu=False, latent=False):
+        self.ctx, self.latent = ctx, latent
+        self.slope, self.end = slope, end_with_relu
+        self.conv1 = ctx.conv(p + ".conv1", 1, latent)
+        self.conv2 = ctx.conv(p + ".conv2", 1, latent)
+
+    def __call__(self, x, y=None, res2=None, scale=None):
+        t = K.conv(self.conv1, x, in_op=IN_LRELU, in_slope=self.slope, act=ACT_LRELU, slope=self.slope)
+        return K.conv(self.conv2, t, y, act=ACT_LRELU if self.end else ACT_NONE, slope=self.slope,
+                      res=x, res2=res2, scale=scale)
+
+
+class UNet:
+    """UNet / UNet2 (video_net.py:129-214) with cat-free skip buffers."""
+
+    def __init__(self, ctx, p, gated=False):
+        self.ctx = ctx
+        B = lambda n: DepthConvBlock(ctx, f"{p}.{n}", gated=gated)  # noqa: E731
+        self.conv1, self.conv2, self.conv3 = B("conv1"), B("conv2"), B("conv3")
+        self.refine = [B(f"context_refine.{i}") for i in range(4)]
+        self.up3 = ctx.conv(p + ".up3.0")
+        self.up_conv3 = B("up_conv3")
+        self.up2 = ctx.conv(p + ".up2.0")
+        self.up_conv2 = B("up_conv2")
+
+    def __call__(self, x, y=None):
+        dt = self.ctx.prec.feat
+        H, W = x.H, x.W
+        c1 = self.conv1.cout
+        c2 = self.conv2.cout
+        cat2 = K.empty(H, W, c1 + self.up2.cout // 4, dt, x.buf.device)
+        x1 = self.conv1(x, cat2.ch(0, c1))
+        x2p = K.pool2x2(x1, True)
+        cat3 = K.empty(H // 2, W // 2, c2 + self.up3.cout // 4, dt, x.buf.device)
+        x2 = self.conv2(x2p, cat3.ch(0, c2))
+        x3 = self.conv3(K.pool2x2(x2, True))
+        for b in self.refine:
+            x3 = b(x3)
+        K.conv(self.up3, x3, cat3.ch(c2, self.up3.cout // 4), shuffle=True)
+        d3 = self.up_conv3(cat3)
+        K.conv(self.up2, d3, cat2.ch(c1, self.up2.cout // 4), shuffle=True)
+        return self.up_conv2(cat2, y)
+
+
+class SpyNet:
+    """ME_Spynet + MEBasic (video_net.py:79-126).  Flows are fp32."""
+
+    def __init__(self, ctx, p, grids):
+        self.ctx, self.grids = ctx, grids
+        self.levels = [[ctx.conv(f"{p}.moduleBasic.{lv}.conv{i}") for i in range(1, 6)] for lv in range(4)]
+
+    def __call__(self, im1, im2):
+        dev = im1.buf.device
+        p1, p2 = [im1], [im2]
+        for _ in range(3):
+            p1.append(K.pool2x2(p1[-1], False))
+            p2.append(K.pool2x2(p2[-1], False))
+        flow = K.zeros(p2[3].H // 2, p2[3].W // 2, 2, F32, dev)
+        cdt = self.ctx.prec.feat_compute
+        in_dt = F32 if cdt == F32 else self.ctx.prec.feat
+        for lv in range(4):
+            k = 3 - lv
+            H, W = p1[k].H, p1[k].W
+            cat = K.empty(H, W, 8, F32, dev)  # [im1 | warp(im2, flow_up) | flow_up]
+            flow_up = K.resize2x(flow, True, 2.0, y=cat.ch(6, 2))
+            K.copy(p1[k], cat.ch(0, 3))
+            K.flow_warp(p2[k], flow_up, self.grids(H, W), y=cat.ch(3, 3))
+            convs = self.levels[lv]
+            t = cast(cat, in_dt)
+            for c in convs[:4]:
+                t = K.conv(c, t, out_dtype=in_dt, act=ACT_LRELU, slope=0.0)
+            flow = K.conv(convs[4], t, out_dtype=F32, res=cast(flow_up, F32) if flow_up.dtype != F32 else flow_up)
+        return flow
+
+
+def hyper_enc(ctx, p, reduce_enc_layer):
+    """get_hyper_enc_dec_models encoder (video_net.py:217-237)."""
+    if reduce_enc_layer:
+        convs = [(ctx.conv(p + ".0", 1, True), True), (ctx.conv(p + ".2", 2, True), True),
+                 (ctx.conv(p + ".4", 2, True), False)]
+    else:
+        convs = [(ctx.conv(p + ".0", 1, True), True), (ctx.conv(p + ".2", 1, True), True),
+                 (ctx.conv(p + ".4", 2, True), True), (ctx.conv(p + ".6", 1, True), True),
+                 (ctx.conv(p + ".8", 2, True), False)]
+
+    def run(x):
+        for c, relu in convs:
+            x = K.conv(c, ctx.fit(x, c.compute), out_dtype=F32, act=ACT_LRELU if relu else K.ACT_ROUND,
+                       slope=0.01)
+        return x  # last conv rounds: z_hat = round(z)
+    return run
+
+
+def hyper_dec(ctx, p):
+    """get_hyper_enc_dec_models decoder (video_net.py:239-249)."""
+    c0, c2, c4, c6, c8 = (ctx.conv(f"{p}.{i}", 1, True) for i in (0, 2, 4, 6, 8))
+
+    def run(x, y=None):
+        x = K.conv(c0, x, act=ACT_LRELU, slope=0.01)
+        x = K.conv(c2, x, shuffle=True, act=ACT_LRELU, slope=0.01)
+        x = K.conv(c4, x, act=ACT_LRELU, slope=0.01)
+        x = K.conv(c6, x, shuffle=True, act=ACT_LRELU, slope=0.01)
+        return K.conv(c8, x, y)
+    return run
+
+
+class Grids:
+    """The reference's cached fp32 linspace grids (video_net.py:11-19),
+    computed once per size on the host with the CPU linspace so the values
+    are those of the CPU reference."""
+
+    def __init__(self, device):
+        self.dev = device
+        self.cache = {}
+
+    def __call__(self, H, W):
+        key = (H, W)
+        if key not in self.cache:
+            gx = torch.linspace(-1.0, 1.0, W, dtype=torch.float32).to(self.dev)
+            gy = torch.linspace(-1.0, 1.0, H, dtype=torch.float32).to(self.dev)
+            self.cache[key] = (gx, gy)
+        return self.cache[key]

@@ -1,0 +1,168 @@
+/*
+ * dcvc_hip.h — C ABI of the gfx950 kernels (libdcvc_hip.so).
+ *
+ * The reference has no kernels of its own: its hot path is stock ATen ops
+ * driven by nn.Modules.  Each entry point here replaces one
+ * family of those ops as the reference uses them, fused with the elementwise
+ * work around it; the citation on each names the reference call sites.
+ *
+ * Conventions
+ *   - Activations are NHWC, batch 1, in HBM.  A tensor argument is a base
+ *     pointer plus (cstride, coff): element (y, x, c) lives at
+ *     base[(y * W + x) * cstride + coff + c].  Writing a conv's output at a
+ *     channel offset of a wider buffer is how torch.cat is expressed.
+ *   - dtype codes: DCVC_F32 (float) or DCVC_BF16 (bfloat16 stored as uint16).
+ *   - Every call is asynchronous on the given hipStream_t (passed as void*).
+ *   - Returns DCVC_HIP_OK or a negative code; shapes are validated on the
+ *     host before launch so a bad call never reaches the GPU.
+ */
+#ifndef DCVC_HIP_H
+#define DCVC_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DCVC_HIP_OK 0
+#define DCVC_HIP_EINVAL (-1)
+#define DCVC_HIP_ELAUNCH (-2)
+#define DCVC_HIP_EUNSUPPORTED (-3)
+
+enum dcvc_dtype { DCVC_F32 = 0, DCVC_BF16 = 1 };
+
+enum dcvc_act {
+  DCVC_ACT_NONE = 0,
+  DCVC_ACT_LRELU = 1,   /* x >= 0 ? x : slope * x (ReLU is slope 0)      */
+  DCVC_ACT_CLAMP01 = 2, /* clamp to [0, 1] (x_hat.clamp_(0, 1))          */
+  DCVC_ACT_ROUND = 3    /* round half to even (torch.round of z)         */
+};
+
+/* Input transform applied while staging the conv input tile. */
+enum dcvc_in_op {
+  DCVC_IN_NONE = 0,
+  DCVC_IN_LRELU = 1, /* lrelu(x, in_slope): ResBlock.first_layer          */
+  DCVC_IN_GATE = 2   /* x[c] * lrelu(x[c + Cin], in_slope): ConvFFN2 gate */
+};
+
+typedef struct dcvc_tensor {
+  void *ptr;
+  int dtype;   /* dcvc_dtype */
+  int H, W, C; /* logical shape of the view */
+  int cstride; /* channels of the underlying buffer */
+  int coff;    /* channel offset of the view */
+} dcvc_tensor;
+
+/*
+ * Dense / strided 2-D convolution as an implicit GEMM on MFMA.
+ * Replaces nn.Conv2d calls of the hot path (kernel 1/2/3/7, stride 1/2,
+ * padding (k-1)//2, groups 1): every conv in DCVC-DC/src/models/video_net.py,
+ * layers.py, video_model.py, image_model.py except the depthwise and grouped
+ * ones.  Fused: input transform (in_op), bias, activation, residual add(s),
+ * per-output-channel scale (the `* quant_step` multiplies), pixel shuffle r=2
+ * on store (subpel_conv*), output dtype conversion.
+ *   out = scale[c] * (res2 + (res + act(conv(in_op(x)) + bias)))
+ * Weights are pre-packed by dcvc_conv_pack_weights.
+ */
+typedef struct dcvc_conv_args {
+  dcvc_tensor x;
+  dcvc_tensor y;          /* H, W = output size after shuffle; C = output channels after shuffle */
+  const void *w;          /* packed weights (see dcvc_conv_pack_weights)   */
+  const float *bias;      /* [Cout] or NULL                                */
+  int cin, cout;          /* conv channels (cout before pixel shuffle)    */
+  int kh, kw, stride, pad;
+  int compute;            /* DCVC_BF16: bf16 MFMA, DCVC_F32: f32 MFMA      */
+  int in_op;              /* dcvc_in_op                                    */
+  float in_slope;
+  int act;                /* dcvc_act                                      */
+  float slope;
+  int shuffle;            /* 1: pixel_shuffle(2) on store                  */
+  const float *scale;     /* per output channel (after shuffle) or NULL    */
+  dcvc_tensor res;        /* ptr NULL when absent; same shape as y         */
+  dcvc_tensor res2;       /* second residual, added after res              */
+} dcvc_conv_args;
+
+/* Pack reference-layout fp32 weights [Cout][Cin][kh][kw] (host pointer) into
+ * the kernel layout [Cout][kh][kw][Cin_pad] (Cin_pad = Cin rounded up to 32)
+ * in dtype `compute`, written to host buffer `out`.  Returns the number of
+ * elements written (Cout*kh*kw*Cin_pad) or a negative code. */
+int64_t dcvc_conv_pack_weights(const float *w, int cout, int cin, int kh,
+                               int kw, int compute, void *out);
+int dcvc_conv2d(const dcvc_conv_args *a, void *stream);
+
+/* Depthwise 3x3 conv, stride 1, padding 1, + bias (DepthConv.depth_conv,
+ * DCVC-DC/src/models/layers.py:143-144).  w: [9][C] fp32 (tap-major). */
+int dcvc_dwconv3x3(dcvc_tensor x, dcvc_tensor y, const float *w,
+                   const float *bias, void *stream);
+
+/* Bilinear backward warp, grid_sample(bilinear, border, align_corners=True)
+ * with the reference's cached fp32 linspace grid (torch_warp,
+ * DCVC-DC/src/models/video_net.py:11-38).  flow: 2 channels fp32 (dx, dy) in
+ * pixels; gx[W], gy[H]: the linspace grid values. */
+int dcvc_flow_warp(dcvc_tensor x, dcvc_tensor flow, dcvc_tensor y,
+                   const float *gx, const float *gy, void *stream);
+
+/* OffsetDiversity after its conv stack (DCVC-DC/src/models/video_model.py:
+ * 45-61): bilinear x2 upsample of the 96-channel offset map, 40*tanh offsets
+ * + flow, sigmoid masks, 32 grouped warps of the 48-channel feature, mask
+ * multiply and the grouped (16 groups) 1x1 fusion conv. fw: [48][6] fp32. */
+int dcvc_offset_diversity(dcvc_tensor feat, dcvc_tensor offs_half,
+                          dcvc_tensor flow, dcvc_tensor y, const float *fw,
+                          const float *fb, const float *gx, const float *gy,
+                          float max_mag, void *stream);
+
+/* Bilinear resize by 2 (up) or 1/2 (down), align_corners=False
+ * (bilinearupsacling / bilineardownsacling, video_net.py:41-55), followed by
+ * a multiply (flow * 2.0, mv / 2). */
+int dcvc_resize2x(dcvc_tensor x, dcvc_tensor y, int up, float mul,
+                  void *stream);
+/* 2x2 stride-2 pooling: avg (ME_Spynet, video_net.py:112) or max (UNet). */
+int dcvc_pool2x2(dcvc_tensor x, dcvc_tensor y, int is_max, void *stream);
+
+/* Generic elementwise over a view: y = a (+ b) (* per-channel scale); or
+ * a dtype-converting copy.  Used for the few cats / adds that are not
+ * fused into a conv. */
+int dcvc_add(dcvc_tensor a, dcvc_tensor b, dcvc_tensor y, void *stream);
+int dcvc_copy(dcvc_tensor x, dcvc_tensor y, void *stream);
+/* Replicate pad / crop of a view into y (pad_for_y / slice_to_y and the
+ * harness's F.pad(replicate), common_model.py:70-86, test_video.py:130). */
+int dcvc_pad_replicate(dcvc_tensor x, dcvc_tensor y, void *stream);
+/* uint8 CHW frame -> float NHWC /255 with replicate padding to y's size. */
+int dcvc_frame_to_nhwc(const uint8_t *src, int h, int w, dcvc_tensor y,
+                       void *stream);
+
+/*
+ * Quadtree (four-part) prior step k, encoder side
+ * (forward_four_part_prior write=True, DCVC-DC/src/models/common_model.py:
+ * 142-252).  y: latent (C ch, fp32); params: common_params (3C ch:
+ * quant_step | scales | means); sm: step scales|means (2C ch) for k > 0
+ * (NULL ptr for k = 0: scales/means come from params).  For the positions of
+ * step k writes: symbols/indexes (int16, NCHW order of the C/4-channel y_q_w_k
+ * tensor, symbols clamped to +-30000) for the coder; y_hat_so_far values
+ * (y_q + means) into yhs (C ch); y_hat * quant_step into yhat (C ch).
+ * Index = build_indexes(scales) with (log_min, log_step).
+ */
+int dcvc_quadtree_encode_step(dcvc_tensor y, dcvc_tensor params,
+                              dcvc_tensor sm, int k, dcvc_tensor yhs,
+                              dcvc_tensor yhat, int16_t *symbols,
+                              int16_t *indexes, float log_min, float log_step,
+                              void *stream);
+/* Decoder side, phase 1: indexes of step k (decompress_four_part_prior
+ * scales_r, common_model.py:274-311). */
+int dcvc_quadtree_indexes_step(dcvc_tensor params, dcvc_tensor sm, int k,
+                               int16_t *indexes, float log_min,
+                               float log_step, void *stream);
+/* Decoder side, phase 2: scatter decoded symbols of step k. */
+int dcvc_quadtree_decode_step(dcvc_tensor params, dcvc_tensor sm, int k,
+                              const int16_t *symbols, dcvc_tensor yhs,
+                              dcvc_tensor yhat, void *stream);
+/* Factorized-prior symbols (BitEstimator.encode, entropy_models.py:184-187):
+ * NHWC float z_hat -> NCHW int16 (clamped +-30000); and the inverse. */
+int dcvc_nhwc_to_symbols(dcvc_tensor x, int16_t *symbols, void *stream);
+int dcvc_symbols_to_nhwc(const int16_t *symbols, dcvc_tensor y, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DCVC_HIP_H */

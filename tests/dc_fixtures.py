@@ -21,7 +21,7 @@ def digest(t):
 
 class DCGolden:
     def __init__(self):
-        with open(os.path.join(GOLDEN, "dc_param_spec.json")) as f:
+        with open(os.path.join(os.path.dirname(GOLDEN), "..", "dcvc_amd", "data", "dc_param_spec.json")) as f:
             spec = json.load(f)
         self.i_spec = [(n, tuple(s)) for n, s in spec["intra"]]
         self.p_spec = [(n, tuple(s)) for n, s in spec["inter"]]

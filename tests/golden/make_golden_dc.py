@@ -205,7 +205,7 @@ def main():
     torch.manual_seed(0)
     i_spec = [(k, list(v.shape)) for k, v in IntraNoAR().state_dict().items()]
     p_spec = [(k, list(v.shape)) for k, v in DMC().state_dict().items()]
-    with open(os.path.join(HERE, "dc_param_spec.json"), "w") as f:
+    with open(os.path.join(REPO, "dcvc_amd", "data", "dc_param_spec.json"), "w") as f:
         json.dump({"intra": i_spec, "inter": p_spec}, f)
     i_sd = synthetic_state_dict(i_spec, seed=0)
     p_sd = synthetic_state_dict(p_spec, seed=1)

@@ -1,0 +1,143 @@
+"""End-to-end DCVC-DC parity on the GPU: the product (dcvc_amd, HIP kernels)
+against the CPU oracle (pinned bit-exact to the reference by
+tests/test_oracle_dc.py) on the golden sequences, in write mode.
+
+Checked per frame:
+  * lossless self-consistency: every symbol the GPU decoder reads equals the
+    symbol the GPU encoder wrote, with identical CDF indexes (bit-exact);
+  * against the oracle: symbol/index agreement, bits and reconstruction.
+    Float convolutions on MFMA sum in a different order than the CPU, and
+    quantisation (round) and scale->index (log, trunc) are discontinuous, so
+    agreement is statistical: parity mode (all-fp32 kernels) must stay within
+    PARITY_TOL, fast mode (bf16 MFMA, fp32 latents) within FAST_TOL.
+Statistics are written to gpurun_out/parity_dc.json.
+"""
+import json
+import os
+import tempfile
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+# max fraction of symbols differing from the oracle, max |bits - oracle| / oracle,
+# max |PSNR - oracle PSNR| in dB (random-weight sequences, PSNR ~6-7 dB)
+PARITY_TOL = {"sym_frac": 2e-3, "bits_rel": 2e-3, "psnr_db": 2e-3}
+FAST_TOL = {"sym_frac": 0.05, "bits_rel": 0.02, "psnr_db": 0.05}
+
+OUT = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "gpurun_out")
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+def psnr(a, b):
+    mse = torch.mean((a - b) ** 2)
+    return (20 * torch.log10(1 / torch.sqrt(mse))).item()
+
+
+@pytest.fixture(scope="module")
+def oracle_runs(dc_golden):
+    from tests.test_oracle_dc import run_oracle_write
+    from oracle import dc_oracle as O
+    from oracle import rans_oracle as R
+    torch.set_num_threads(min(16, os.cpu_count() or 1))
+    i = O.IntraOracle(dc_golden.i_state_dict(), R.pmf_to_quantized_cdf)
+    p = O.DMCOracle(dc_golden.p_state_dict(), R.pmf_to_quantized_cdf)
+    runs = {}
+    for tag in ("A", "B"):
+        meta = dc_golden.meta[tag]
+        frames = []
+        for t, calls, coder_calls, stream, dpb in run_oracle_write(dc_golden, (i, p), tag):
+            x, _ = dc_golden.frame_tensor(tag, t)
+            hdr = 13 if t == 0 else 6
+            rec = dpb["ref_frame"][:, :, :meta["h"], :meta["w"]]
+            frames.append({"syms": [c[0] for c in coder_calls], "idx": [c[1] for c in coder_calls],
+                           "bits": (len(stream) + hdr) * 8, "psnr": psnr(rec, x), "recon": rec})
+        runs[tag] = frames
+    return runs
+
+
+def run_product(dc_golden, tag, prec):
+    from dcvc_amd.dc import DMC, IntraNoAR
+    meta = dc_golden.meta[tag]
+    h, w, q = meta["h"], meta["w"], meta["q_index"]
+    inet = IntraNoAR(precision=prec).load_state_dict(dc_golden.i_state_dict())
+    pnet = DMC(precision=prec).load_state_dict(dc_golden.p_state_dict())
+    inet.update(force=True)
+    pnet.update(force=True)
+    out = []
+    dpb = None
+    with tempfile.TemporaryDirectory() as td:
+        for t in range(meta["frames"]):
+            x, xp = dc_golden.frame_tensor(tag, t)
+            xp = xp.cuda()
+            net = inet if t == 0 else pnet
+            net.entropy_coder.trace = []
+            path = os.path.join(td, f"{t}.bin")
+            if t == 0:
+                r = inet.encode_decode(xp, False, q, path, pic_width=w, pic_height=h)
+                dpb = {"ref_frame": r["x_hat"], "ref_feature": None, "ref_mv_feature": None,
+                       "ref_y": None, "ref_mv_y": None}
+            else:
+                r = pnet.encode_decode(xp, dpb, False, q, path, pic_width=w, pic_height=h, frame_idx=t % 4)
+                dpb = r["dpb"]
+            tr = net.entropy_coder.trace
+            enc = [e for e in tr if e[0] == "enc"]
+            dec = [e for e in tr if e[0] == "dec"]
+            rec = dpb["ref_frame"].nchw().cpu()[:, :, :h, :w]
+            out.append({"enc": enc, "dec": dec, "bits": r["bit"], "psnr": psnr(rec, x), "recon": rec})
+    return out
+
+
+def compare(prod, orc):
+    stats = []
+    for t, (a, b) in enumerate(zip(prod, orc)):
+        # self-consistency: decoder symbols/indexes == encoder symbols/indexes
+        assert len(a["enc"]) == len(a["dec"]) == len(b["syms"])
+        for (_, s_e, i_e), (_, s_d, i_d) in zip(a["enc"], a["dec"]):
+            np.testing.assert_array_equal(i_e.reshape(-1), i_d.reshape(-1))
+            np.testing.assert_array_equal(s_e.reshape(-1), s_d.reshape(-1))
+        n = sum(s.size for s in b["syms"])
+        ds = sum(int((e[1].reshape(-1) != s.reshape(-1)).sum()) for e, s in zip(a["enc"], b["syms"]))
+        di = sum(int((e[2].reshape(-1) != s.reshape(-1)).sum()) for e, s in zip(a["enc"], b["idx"]))
+        stats.append({"t": t, "symbols": n, "sym_diff": ds, "idx_diff": di, "bits": a["bits"],
+                      "bits_oracle": b["bits"], "psnr": a["psnr"], "psnr_oracle": b["psnr"],
+                      "recon_maxabs": float((a["recon"] - b["recon"]).abs().max())})
+    return stats
+
+
+def check(stats, tol):
+    for s in stats:
+        assert s["sym_diff"] / s["symbols"] <= tol["sym_frac"], s
+        assert abs(s["bits"] - s["bits_oracle"]) / s["bits_oracle"] <= tol["bits_rel"], s
+        assert abs(s["psnr"] - s["psnr_oracle"]) <= tol["psnr_db"], s
+
+
+def _dump(name, stats):
+    os.makedirs(OUT, exist_ok=True)
+    path = os.path.join(OUT, "parity_dc.json")
+    d = json.load(open(path)) if os.path.exists(path) else {}
+    d[name] = stats
+    json.dump(d, open(path, "w"), indent=1)
+
+
+@pytest.mark.parametrize("tag", ["B", "A"])
+def test_parity_mode_vs_oracle(dc_golden, oracle_runs, tag):
+    from dcvc_amd.layers import Precision
+    stats = compare(run_product(dc_golden, tag, Precision.parity()), oracle_runs[tag])
+    _dump(f"parity_{tag}", stats)
+    check(stats, PARITY_TOL)
+
+
+@pytest.mark.parametrize("tag", ["B", "A"])
+def test_fast_mode_vs_oracle(dc_golden, oracle_runs, tag):
+    from dcvc_amd.layers import Precision
+    stats = compare(run_product(dc_golden, tag, Precision.fast()), oracle_runs[tag])
+    _dump(f"fast_{tag}", stats)
+    check(stats, FAST_TOL)
