@@ -42,6 +42,7 @@ def parse():
     ap.add_argument("--stream_part", type=int, default=1)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--profile-out", default="", help="per-shape kernel timing JSON of one P-frame")
     return ap.parse_args()
 
 
@@ -141,7 +142,7 @@ def main():
     from dcvc_amd.synth import moving_pattern
 
     isd, psd = make_weights(dist, rank, device)
-    prec = Precision.fast() if args.precision == "fast" else Precision.parity()
+    prec = Precision.fast(latent_compute=K.BF16) if args.precision == "fast" else Precision.parity()
     inet = IntraNoAR(precision=prec, stream_part=args.stream_part, device=device).load_state_dict(isd)
     pnet = DMC(precision=prec, stream_part=args.stream_part, device=device).load_state_dict(psd)
     inet.update(force=True)
@@ -200,14 +201,22 @@ def main():
         K.PROFILE = []
         step(nframes - 1 if (nframes - 1) % args.gop else nframes - 2)
         torch.cuda.synchronize(device)
-        fam = {}
-        for f, e0, e1, fl, nb in K.PROFILE:
-            d = fam.setdefault(f, [0.0, 0, 0, 0])
-            d[0] += e0.elapsed_time(e1) * 1e-3
-            d[1] += fl
-            d[2] += nb
-            d[3] += 1
+        fam, shapes = {}, {}
+        for f, e0, e1, fl, nb, key in K.PROFILE:
+            dt = e0.elapsed_time(e1) * 1e-3
+            for tab, k in ((fam, f), (shapes, f + " " + key)):
+                d = tab.setdefault(k, [0.0, 0, 0, 0])
+                d[0] += dt
+                d[1] += fl
+                d[2] += nb
+                d[3] += 1
         K.PROFILE = None
+        if args.profile_out:
+            rows = sorted(shapes.items(), key=lambda kv: -kv[1][0])
+            with open(args.profile_out, "w") as f:
+                json.dump([{"op": k, "ms": round(v[0] * 1e3, 4), "n": v[3],
+                            "tflops": round(v[1] / max(v[0], 1e-12) / 1e12, 2),
+                            "gbs": round(v[2] / max(v[0], 1e-12) / 1e9, 1)} for k, v in rows], f, indent=0)
         dom = max(fam, key=lambda k: fam[k][0])
         tsec, fl, nb, n = fam[dom]
         if dom == "conv":

@@ -46,6 +46,9 @@ struct ConvP {
   int r2cs, r2co;
   int Wout;  // width of y buffer (after shuffle)
   int tiles_x, tiles_y;
+  int vec;      // 16-byte input staging allowed (channel alignment)
+  int vec_out;  // 4-channel vector epilogue allowed (no shuffle, alignment)
+  int wall;     // stage all kernel rows' weights per chunk
 };
 
 // LDS image helpers ---------------------------------------------------------
@@ -70,73 +73,181 @@ __device__ __forceinline__ float load_in(const ConvP &p, int gy, int gx, int c) 
   return v;
 }
 
-template <typename TIN, bool F32, int TH>
+// 8 consecutive input channels starting at element offset e (16-byte aligned)
+__device__ __forceinline__ void load8(const float *x, int64_t e, float v[8]) {
+  const float4 a = *reinterpret_cast<const float4 *>(x + e);
+  const float4 b = *reinterpret_cast<const float4 *>(x + e + 4);
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+  v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+__device__ __forceinline__ void load8(const uint16_t *x, int64_t e, float v[8]) {
+  const u16x8 a = *reinterpret_cast<const u16x8 *>(x + e);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = bf2f(a[j]);
+}
+
+// Input tile staging.  One work item = one pixel x 8 channels (a 16-byte LDS
+// slot).  Items are processed in groups of kU per thread: all kU global loads
+// are issued before any LDS store, so kU loads are in flight per thread.
+constexpr int kU = 4;
+
+template <typename TIN, bool F32>
 __device__ __forceinline__ void stage_input(const ConvP &p, void *lds_in, int ch0,
                                             int iy0, int ix0, int IH, int IW,
                                             int IWp) {
-  // 8 channels per work item
   const int items = IH * IW * 4;
-  for (int it = threadIdx.x; it < items; it += 256) {
-    const int slot = it & 3;
-    const int pix = it >> 2;
-    const int iy = pix / IW, ix = pix - iy * IW;
-    const int gy = iy0 + iy, gx = ix0 + ix;
-    float v[8];
-    const bool inb = gy >= 0 && gy < p.H && gx >= 0 && gx < p.W;
+  const TIN *X = reinterpret_cast<const TIN *>(p.x);
+  for (int base = threadIdx.x; base < items; base += 256 * kU) {
+    float v[kU][8];
+    int rows[kU];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int c = ch0 + slot * 8 + j;
-      v[j] = (inb && c < p.cin) ? load_in<TIN>(p, gy, gx, c) : 0.f;
+    for (int u = 0; u < kU; ++u) {
+      const int it = base + u * 256;
+      rows[u] = -1;
+      if (it >= items) continue;
+      const int slot = it & 3;
+      const int pix = it >> 2;
+      const int iy = pix / IW, ix = pix - iy * IW;
+      const int gy = iy0 + iy, gx = ix0 + ix;
+      const int c0 = ch0 + slot * 8;
+      rows[u] = (iy * IWp + ix) * 4 + slot;
+      const bool inb = gy >= 0 && gy < p.H && gx >= 0 && gx < p.W && c0 < p.cin;
+      if (p.vec) {
+        if (inb) {
+          const int64_t e = ((int64_t)gy * p.W + gx) * p.xcs + p.xco + c0;
+          load8(X, e, v[u]);
+          if (p.in_op == DCVC_IN_GATE) {
+            float g[8];
+            load8(X, e + p.cin, g);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[u][j] = v[u][j] * (g[j] >= 0.f ? g[j] : g[j] * p.in_slope);
+          }
+        } else {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[u][j] = 0.f;
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int c = c0 + j;
+          v[u][j] = (inb && c < p.cin) ? load_in<TIN>(p, gy, gx, c) : 0.f;
+        }
+      }
     }
-    const int row = iy * IWp + ix;
-    if constexpr (F32) {
-      float *L = reinterpret_cast<float *>(lds_in);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) L[off_f32(row, slot * 8 + j)] = v[j];
-    } else {
-      u16x8 pk;
+    for (int u = 0; u < kU; ++u) {
+      if (rows[u] < 0) continue;
+      if (p.vec && p.in_op == DCVC_IN_LRELU) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) pk[j] = f2bf(v[j]);
-      *reinterpret_cast<u16x8 *>(reinterpret_cast<uint16_t *>(lds_in) + swz_off_bf16(row, slot)) = pk;
+        for (int j = 0; j < 8; ++j) v[u][j] = v[u][j] >= 0.f ? v[u][j] : v[u][j] * p.in_slope;
+      }
+      const int row = rows[u] >> 2, slot = rows[u] & 3;
+      if constexpr (F32) {
+        float *L = reinterpret_cast<float *>(lds_in);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) L[off_f32(row, slot * 8 + j)] = v[u][j];
+      } else {
+        u16x8 pk;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) pk[j] = f2bf(v[u][j]);
+        *reinterpret_cast<u16x8 *>(reinterpret_cast<uint16_t *>(lds_in) + swz_off_bf16(row, slot)) = pk;
+      }
     }
   }
 }
 
+// Stage weights of kernel rows [dy0, dy0 + ndy) of one channel chunk; LDS
+// row index = ((dy - dy0) * kw + dx) * BN + n.  Batched like stage_input.
 template <bool F32, int BN>
 __device__ __forceinline__ void stage_weights(const ConvP &p, void *lds_w, int n0,
-                                              int chunk, int dy) {
-  const int items = p.kw * BN * 4;  // 8-channel pieces
-  for (int it = threadIdx.x; it < items; it += 256) {
-    const int slot = it & 3;
-    const int rr = it >> 2;  // rr = dx * BN + nn
-    const int dx = rr / BN, nn = rr - dx * BN;
-    const int n = n0 + nn;
-    const int64_t src = (((int64_t)n * p.kh + dy) * p.kw + dx) * p.cinp + chunk * kChunk + slot * 8;
+                                              int chunk, int dy0, int ndy) {
+  const int items = ndy * p.kw * BN * 4;  // 8-channel pieces
+  for (int base = threadIdx.x; base < items; base += 256 * kU) {
+    int rrs[kU];
     if constexpr (F32) {
-      float *L = reinterpret_cast<float *>(lds_w);
+      float4 va[kU], vb[kU];
       const float *W = reinterpret_cast<const float *>(p.w);
-      if (n < p.cout) {
-        const float4 a = *reinterpret_cast<const float4 *>(W + src);
-        const float4 b = *reinterpret_cast<const float4 *>(W + src + 4);
-        float *d = L + off_f32(rr, slot * 8);
-        d[0] = a.x; d[1] = a.y; d[2] = a.z; d[3] = a.w;
-        d[4] = b.x; d[5] = b.y; d[6] = b.z; d[7] = b.w;
-      } else {
-        float *d = L + off_f32(rr, slot * 8);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) d[j] = 0.f;
+      for (int u = 0; u < kU; ++u) {
+        const int it = base + u * 256;
+        rrs[u] = -1;
+        if (it >= items) continue;
+        const int slot = it & 3, rr = it >> 2;
+        const int tap = rr / BN, nn = rr - tap * BN;
+        const int n = n0 + nn;
+        rrs[u] = it;
+        if (n < p.cout) {
+          const int64_t src = (((int64_t)n * p.kh + dy0 + tap / p.kw) * p.kw + tap % p.kw) * p.cinp +
+                              chunk * kChunk + slot * 8;
+          va[u] = *reinterpret_cast<const float4 *>(W + src);
+          vb[u] = *reinterpret_cast<const float4 *>(W + src + 4);
+        } else {
+          va[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+          vb[u] = va[u];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        if (rrs[u] < 0) continue;
+        float *d = reinterpret_cast<float *>(lds_w) + off_f32(rrs[u] >> 2, (rrs[u] & 3) * 8);
+        d[0] = va[u].x; d[1] = va[u].y; d[2] = va[u].z; d[3] = va[u].w;
+        d[4] = vb[u].x; d[5] = vb[u].y; d[6] = vb[u].z; d[7] = vb[u].w;
       }
     } else {
-      u16x8 v;
-      if (n < p.cout) {
-        v = *reinterpret_cast<const u16x8 *>(reinterpret_cast<const uint16_t *>(p.w) + src);
-      } else {
+      u16x8 v[kU];
+      const uint16_t *W = reinterpret_cast<const uint16_t *>(p.w);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = 0;
+      for (int u = 0; u < kU; ++u) {
+        const int it = base + u * 256;
+        rrs[u] = -1;
+        if (it >= items) continue;
+        const int slot = it & 3, rr = it >> 2;
+        const int tap = rr / BN, nn = rr - tap * BN;
+        const int n = n0 + nn;
+        rrs[u] = it;
+        if (n < p.cout) {
+          const int64_t src = (((int64_t)n * p.kh + dy0 + tap / p.kw) * p.kw + tap % p.kw) * p.cinp +
+                              chunk * kChunk + slot * 8;
+          v[u] = *reinterpret_cast<const u16x8 *>(W + src);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[u][j] = 0;
+        }
       }
-      *reinterpret_cast<u16x8 *>(reinterpret_cast<uint16_t *>(lds_w) + swz_off_bf16(rr, slot)) = v;
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        if (rrs[u] < 0) continue;
+        *reinterpret_cast<u16x8 *>(reinterpret_cast<uint16_t *>(lds_w) + swz_off_bf16(rrs[u] >> 2, rrs[u] & 3)) =
+            v[u];
+      }
     }
   }
+}
+
+template <typename TOUT>
+__device__ __forceinline__ void store4(const ConvP &p, int64_t pix, int c, const float v[4]);
+template <>
+__device__ __forceinline__ void store4<float>(const ConvP &p, int64_t pix, int c, const float v[4]) {
+  *reinterpret_cast<float4 *>(reinterpret_cast<float *>(p.y) + pix * p.ycs + p.yco + c) =
+      make_float4(v[0], v[1], v[2], v[3]);
+}
+template <>
+__device__ __forceinline__ void store4<uint16_t>(const ConvP &p, int64_t pix, int c, const float v[4]) {
+  u16x4 o;
+  o[0] = f2bf(v[0]); o[1] = f2bf(v[1]); o[2] = f2bf(v[2]); o[3] = f2bf(v[3]);
+  *reinterpret_cast<u16x4 *>(reinterpret_cast<uint16_t *>(p.y) + pix * p.ycs + p.yco + c) = o;
+}
+template <typename T>
+__device__ __forceinline__ void load4(const void *base, int64_t e, float v[4]);
+template <>
+__device__ __forceinline__ void load4<float>(const void *base, int64_t e, float v[4]) {
+  const float4 a = *reinterpret_cast<const float4 *>(reinterpret_cast<const float *>(base) + e);
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+}
+template <>
+__device__ __forceinline__ void load4<uint16_t>(const void *base, int64_t e, float v[4]) {
+  const u16x4 a = *reinterpret_cast<const u16x4 *>(reinterpret_cast<const uint16_t *>(base) + e);
+  v[0] = bf2f(a[0]); v[1] = bf2f(a[1]); v[2] = bf2f(a[2]); v[3] = bf2f(a[3]);
 }
 
 template <typename TIN, typename TOUT, bool F32, int BN, int TH>
@@ -171,15 +282,18 @@ __global__ void __launch_bounds__(256) conv_kernel(ConvP p) {
   const int nchunks = p.cinp / kChunk;
   const int iy0 = oy0 * S - p.pad, ix0 = ox0 * S - p.pad;
   const int col = lane & 15, hi = lane >> 4;
+  const int ndy = p.wall ? p.kh : 1;  // kernel rows staged at once
 
   for (int ch = 0; ch < nchunks; ++ch) {
     __syncthreads();
-    stage_input<TIN, F32, TH>(p, lds_in, ch * kChunk, iy0, ix0, IH, IW, IWp);
-    for (int dy = 0; dy < p.kh; ++dy) {
+    stage_input<TIN, F32>(p, lds_in, ch * kChunk, iy0, ix0, IH, IW, IWp);
+    for (int dy0 = 0; dy0 < p.kh; dy0 += ndy) {
+      if (dy0 > 0) __syncthreads();
+      stage_weights<F32, BN>(p, lds_w, n0, ch, dy0, ndy);
       __syncthreads();
-      stage_weights<F32, BN>(p, lds_w, n0, ch, dy);
-      __syncthreads();
-      for (int dx = 0; dx < p.kw; ++dx) {
+      for (int t = 0; t < ndy * p.kw; ++t) {
+        const int dy = dy0 + t / p.kw, dx = t % p.kw;
+        const int wrow = t * BN;
         if constexpr (F32) {
           const float *Li = reinterpret_cast<const float *>(lds_in);
           const float *Lw = reinterpret_cast<const float *>(lds_w);
@@ -188,7 +302,7 @@ __global__ void __launch_bounds__(256) conv_kernel(ConvP p) {
             const int k = s4 * 4 + hi;
             float a[NT], bb[RW];
 #pragma unroll
-            for (int j = 0; j < NT; ++j) a[j] = Lw[off_f32(dx * BN + j * 16 + col, k)];
+            for (int j = 0; j < NT; ++j) a[j] = Lw[off_f32(wrow + j * 16 + col, k)];
 #pragma unroll
             for (int r = 0; r < RW; ++r) {
               const int row = ((wave * RW + r) * S + dy) * IWp + col * S + dx;
@@ -206,7 +320,7 @@ __global__ void __launch_bounds__(256) conv_kernel(ConvP p) {
           bf16x8 a[NT], bb[RW];
 #pragma unroll
           for (int j = 0; j < NT; ++j)
-            a[j] = *reinterpret_cast<const bf16x8 *>(Lw + swz_off_bf16(dx * BN + j * 16 + col, hi));
+            a[j] = *reinterpret_cast<const bf16x8 *>(Lw + swz_off_bf16(wrow + j * 16 + col, hi));
 #pragma unroll
           for (int r = 0; r < RW; ++r) {
             const int row = ((wave * RW + r) * S + dy) * IWp + col * S + dx;
@@ -231,13 +345,42 @@ __global__ void __launch_bounds__(256) conv_kernel(ConvP p) {
     if (oy >= p.Ho) continue;
 #pragma unroll
     for (int j = 0; j < NT; ++j) {
+      const int nb = n0 + j * 16 + hi * 4;
+      if (nb >= p.cout) continue;
+      float v[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const int n = n0 + j * 16 + hi * 4 + i;
+        const int n = nb + i;
+        float t = acc[r][j][i];
+        if (p.bias && n < p.cout) t += p.bias[n];
+        v[i] = apply_act(p.act, t, p.slope);
+      }
+      if (p.vec_out && nb + 3 < p.cout) {
+        const int64_t pix = (int64_t)oy * p.Wout + ox;
+        if (p.res) {
+          float rv[4];
+          load4<TOUT>(p.res, pix * p.rcs + p.rco + nb, rv);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) v[i] = rv[i] + v[i];
+        }
+        if (p.res2) {
+          float rv[4];
+          load4<TOUT>(p.res2, pix * p.r2cs + p.r2co + nb, rv);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) v[i] = rv[i] + v[i];
+        }
+        if (p.scale) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) v[i] = v[i] * p.scale[nb + i];
+        }
+        store4<TOUT>(p, pix, nb, v);
+        continue;
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int n = nb + i;
         if (n >= p.cout) continue;
-        float v = acc[r][j][i];
-        if (p.bias) v += p.bias[n];
-        v = apply_act(p.act, v, p.slope);
+        float t = v[i];
         int c = n, yy = oy, xx = ox;
         if (p.shuffle) {
           c = n >> 2;
@@ -245,13 +388,24 @@ __global__ void __launch_bounds__(256) conv_kernel(ConvP p) {
           xx = ox * 2 + (n & 1);
         }
         const int64_t pix = (int64_t)yy * p.Wout + xx;
-        if (p.res) v = ld<TOUT>(p.res, pix * p.rcs + p.rco + c) + v;
-        if (p.res2) v = ld<TOUT>(p.res2, pix * p.r2cs + p.r2co + c) + v;
-        if (p.scale) v = v * p.scale[c];
-        st<TOUT>(p.y, pix * p.ycs + p.yco + c, v);
+        if (p.res) t = ld<TOUT>(p.res, pix * p.rcs + p.rco + c) + t;
+        if (p.res2) t = ld<TOUT>(p.res2, pix * p.r2cs + p.r2co + c) + t;
+        if (p.scale) t = t * p.scale[c];
+        st<TOUT>(p.y, pix * p.ycs + p.yco + c, t);
       }
     }
   }
+}
+
+template <bool F32, int BN, int TH>
+size_t lds_bytes(const ConvP &p, bool wall) {
+  const int IH = (TH - 1) * p.s + p.kh;
+  const int IW = 15 * p.s + p.kw;
+  const int IWp = (IW + 3) & ~3;
+  const size_t row = F32 ? 33 * 4 : 32 * 2;
+  const size_t in_bytes = (size_t)IH * IWp * row;
+  const size_t w_bytes = (size_t)(wall ? p.kh : 1) * p.kw * BN * row;
+  return ((in_bytes + 15) & ~(size_t)15) + w_bytes;
 }
 
 template <typename TIN, typename TOUT, bool F32, int BN, int TH>
@@ -260,12 +414,9 @@ int launch(const ConvP &p0, hipStream_t st) {
   p.tiles_x = (p.Wo + 15) / 16;
   p.tiles_y = (p.Ho + TH - 1) / TH;
   const int tiles_n = (p.cout + BN - 1) / BN;
-  const int IH = (TH - 1) * p.s + p.kh;
-  const int IW = 15 * p.s + p.kw;
-  const int IWp = (IW + 3) & ~3;
-  const size_t in_bytes = (size_t)IH * IWp * (F32 ? 33 * 4 : 32 * 2);
-  const size_t w_bytes = (size_t)p.kw * BN * (F32 ? 33 * 4 : 32 * 2);
-  const size_t lds = ((in_bytes + 15) & ~(size_t)15) + w_bytes;
+  // stage every kernel row's weights at once when that keeps LDS modest
+  p.wall = lds_bytes<F32, BN, TH>(p, true) <= 64 * 1024 ? 1 : 0;
+  const size_t lds = lds_bytes<F32, BN, TH>(p, p.wall);
   if (lds > 160 * 1024) return DCVC_HIP_EUNSUPPORTED;
   const int64_t blocks = (int64_t)p.tiles_x * p.tiles_y * tiles_n;
   if (blocks <= 0) return DCVC_HIP_OK;
@@ -279,14 +430,46 @@ int launch(const ConvP &p0, hipStream_t st) {
   return DCVC_HIP_OK;
 }
 
+// Tile choice: BN covers Cout in the fewest n-tiles (max 128); TH shrinks
+// from 16 (8 when strided) to 4 until the grid has >= 1024 workgroups, so
+// the small latent-resolution GEMMs still fill the 256 CUs.
+template <typename TIN, typename TOUT, bool F32, int BN>
+int pick_th(const ConvP &p, hipStream_t st) {
+  const int64_t tx = (p.Wo + 15) / 16, tn = (p.cout + BN - 1) / BN;
+  auto blocks = [&](int th) { return tx * ((p.Ho + th - 1) / th) * tn; };
+  int th = (p.s > 1 || BN > 64) ? 8 : 16;
+  while (th > 4 && blocks(th) < 1024) th /= 2;
+  if (th == 16 && BN <= 64 && lds_bytes<F32, BN, 16>(p, false) <= 160 * 1024)
+    return launch<TIN, TOUT, F32, BN, 16>(p, st);
+  if (th >= 8) return launch<TIN, TOUT, F32, BN, 8>(p, st);
+  return launch<TIN, TOUT, F32, BN, 4>(p, st);
+}
+
+// BN: the n-tile width (multiple of 16) that wastes the fewest MFMA columns,
+// preferring wider tiles on ties; 7x7 kernels stay <= 64 for LDS.
 template <typename TIN, typename TOUT, bool F32>
 int pick_bn(const ConvP &p, hipStream_t st) {
-  const bool strided = p.s > 1;
-  if (p.cout <= 16)
-    return strided ? launch<TIN, TOUT, F32, 16, 8>(p, st) : launch<TIN, TOUT, F32, 16, 16>(p, st);
-  if (p.cout <= 32)
-    return strided ? launch<TIN, TOUT, F32, 32, 8>(p, st) : launch<TIN, TOUT, F32, 32, 16>(p, st);
-  return strided ? launch<TIN, TOUT, F32, 64, 8>(p, st) : launch<TIN, TOUT, F32, 64, 16>(p, st);
+  static const int cand[6] = {16, 32, 48, 64, 96, 128};
+  int best = 16;
+  long best_pad = -1;
+  for (int i = 0; i < 6; ++i) {
+    const int bn = cand[i];
+    if (p.kh * p.kw > 9 && bn > 64) continue;
+    const long tiles = (p.cout + bn - 1) / bn;
+    const long pad = tiles * bn - p.cout;
+    if (best_pad < 0 || pad < best_pad || (pad == best_pad && bn > best)) {
+      best = bn;
+      best_pad = pad;
+    }
+  }
+  switch (best) {
+    case 16: return pick_th<TIN, TOUT, F32, 16>(p, st);
+    case 32: return pick_th<TIN, TOUT, F32, 32>(p, st);
+    case 48: return pick_th<TIN, TOUT, F32, 48>(p, st);
+    case 64: return pick_th<TIN, TOUT, F32, 64>(p, st);
+    case 96: return pick_th<TIN, TOUT, F32, 96>(p, st);
+    default: return pick_th<TIN, TOUT, F32, 128>(p, st);
+  }
 }
 
 bool valid_view(const dcvc_tensor &t) {
@@ -375,6 +558,16 @@ extern "C" int dcvc_conv2d(const dcvc_conv_args *a, void *stream) {
   }
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const bool xin32 = a->x.dtype == DCVC_F32, yout32 = a->y.dtype == DCVC_F32;
+  {
+    const int xa = xin32 ? 4 : 8;   // elements per 16 bytes
+    p.vec = (a->cin % 8 == 0) && (p.xcs % xa == 0) && (p.xco % xa == 0) &&
+            ((uintptr_t)p.x % 16 == 0);
+    const int ya = yout32 ? 4 : 4;  // 4 channels per vector store
+    bool vo = !a->shuffle && (p.ycs % ya == 0) && (p.yco % ya == 0) && ((uintptr_t)p.y % 16 == 0);
+    if (a->res.ptr) vo = vo && (p.rcs % 4 == 0) && (p.rco % 4 == 0);
+    if (a->res2.ptr) vo = vo && (p.r2cs % 4 == 0) && (p.r2co % 4 == 0);
+    p.vec_out = vo ? 1 : 0;
+  }
   if (a->compute == DCVC_F32) {
     if (!xin32 || !yout32) return DCVC_HIP_EUNSUPPORTED;
     return pick_bn<float, float, true>(p, st);

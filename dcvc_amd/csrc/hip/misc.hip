@@ -48,6 +48,64 @@ __global__ void dw_kernel(View x, View y, const float *w, const float *b) {
   st<TY>(y.p, pix * y.cs + y.co + c, acc + b[c]);
 }
 
+// 8 channels per thread, 16-byte loads/stores (C % 8 == 0, aligned views)
+template <typename T> struct V8;
+template <> struct V8<uint16_t> {
+  __device__ __forceinline__ static void load(const void *b, int64_t e, float v[8]) {
+    const u16x8 a = *reinterpret_cast<const u16x8 *>(reinterpret_cast<const uint16_t *>(b) + e);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = bf2f(a[j]);
+  }
+  __device__ __forceinline__ static void store(void *b, int64_t e, const float v[8]) {
+    u16x8 a;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) a[j] = f2bf(v[j]);
+    *reinterpret_cast<u16x8 *>(reinterpret_cast<uint16_t *>(b) + e) = a;
+  }
+};
+template <> struct V8<float> {
+  __device__ __forceinline__ static void load(const void *b, int64_t e, float v[8]) {
+    const float4 x = *reinterpret_cast<const float4 *>(reinterpret_cast<const float *>(b) + e);
+    const float4 y = *reinterpret_cast<const float4 *>(reinterpret_cast<const float *>(b) + e + 4);
+    v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w; v[4] = y.x; v[5] = y.y; v[6] = y.z; v[7] = y.w;
+  }
+  __device__ __forceinline__ static void store(void *b, int64_t e, const float v[8]) {
+    *reinterpret_cast<float4 *>(reinterpret_cast<float *>(b) + e) = make_float4(v[0], v[1], v[2], v[3]);
+    *reinterpret_cast<float4 *>(reinterpret_cast<float *>(b) + e + 4) = make_float4(v[4], v[5], v[6], v[7]);
+  }
+};
+
+template <typename TX, typename TY>
+__global__ void dw8_kernel(View x, View y, const float *w, const float *b) {
+  const int cg = y.C >> 3;
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (int64_t)y.H * y.W * cg) return;
+  const int c = (int)(idx % cg) * 8;
+  const int64_t pix = idx / cg;
+  const int py = (int)(pix / y.W), px = (int)(pix - (int64_t)py * y.W);
+  float acc[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+#pragma unroll
+  for (int dy = -1; dy <= 1; ++dy) {
+    const int yy = py + dy;
+    if (yy < 0 || yy >= x.H) continue;
+#pragma unroll
+    for (int dx = -1; dx <= 1; ++dx) {
+      const int xx = px + dx;
+      if (xx < 0 || xx >= x.W) continue;
+      float v[8];
+      V8<TX>::load(x.p, ((int64_t)yy * x.W + xx) * x.cs + x.co + c, v);
+      const float *wt = w + ((dy + 1) * 3 + dx + 1) * y.C + c;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += wt[j] * v[j];
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) acc[j] += b[c + j];
+  V8<TY>::store(y.p, pix * y.cs + y.co + c, acc);
+}
+
 // ------------------------------------------------------------ elementwise
 template <typename TA, typename TY>
 __global__ void add_kernel(View a, View b, int b32, View y) {
@@ -218,10 +276,19 @@ extern "C" int dcvc_dwconv3x3(dcvc_tensor x, dcvc_tensor y, const float *w, cons
                               void *stream) {
   if (!ok(x) || !ok(y) || !w || !bias || x.C != y.C || x.H != y.H || x.W != y.W) return DCVC_HIP_EINVAL;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  const unsigned g = blocks_for((int64_t)y.H * y.W * y.C);
-#define K(TX, TY) hipLaunchKernelGGL((dw_kernel<TX, TY>), dim3(g), dim3(256), 0, st, mk(x), mk(y), w, bias)
-  DISPATCH2(x.dtype, y.dtype, K);
+  const bool vec = (x.C % 8 == 0) && (x.cstride % 8 == 0) && (x.coff % 8 == 0) && (y.cstride % 8 == 0) &&
+                   (y.coff % 8 == 0);
+  if (vec) {
+    const unsigned g = blocks_for((int64_t)y.H * y.W * (y.C / 8));
+#define K(TX, TY) hipLaunchKernelGGL((dw8_kernel<TX, TY>), dim3(g), dim3(256), 0, st, mk(x), mk(y), w, bias)
+    DISPATCH2(x.dtype, y.dtype, K);
 #undef K
+  } else {
+    const unsigned g = blocks_for((int64_t)y.H * y.W * y.C);
+#define K(TX, TY) hipLaunchKernelGGL((dw_kernel<TX, TY>), dim3(g), dim3(256), 0, st, mk(x), mk(y), w, bias)
+    DISPATCH2(x.dtype, y.dtype, K);
+#undef K
+  }
   DCVC_LAUNCH_CHECK();
   return DCVC_HIP_OK;
 }

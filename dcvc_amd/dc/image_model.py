@@ -56,6 +56,8 @@ class IntraNoAR:
         self.refine_conv = ctx.conv("refine.1")
         self.fine = {k: q_fine(sd[k]) for k in ("q_scale_enc", "q_scale_dec")}
         self._q_cache = {}
+        if strict:
+            ctx.check_strict([k for k in sd if k.startswith("bit_estimator") or k.startswith("q_")])
         return self
 
     def update(self, force=False):

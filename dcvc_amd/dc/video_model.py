@@ -52,8 +52,8 @@ class DMC:
         self.off_c0 = ctx.conv("align.conv_offset.0", 2)
         self.off_c2 = ctx.conv("align.conv_offset.2")
         self.off_c4 = ctx.conv("align.conv_offset.4")
-        self.fusion_w = sd["align.fusion.weight"].detach().float().reshape(48, 6).contiguous().to(self.dev)
-        self.fusion_b = sd["align.fusion.bias"].detach().float().contiguous().to(self.dev)
+        self.fusion_w = ctx.take("align.fusion.weight").detach().float().reshape(48, 6).contiguous().to(self.dev)
+        self.fusion_b = ctx.take("align.fusion.bias").detach().float().contiguous().to(self.dev)
         # MvEnc (video_model.py:121-146)
         self.me1 = ResidualBlockWithStride(ctx, "mv_encoder.enc_1.0")
         self.me1b = DepthConvBlock(ctx, "mv_encoder.enc_1.1")
@@ -121,7 +121,8 @@ class DMC:
         self.fine = {k: q_fine(sd[k]) for k in
                      ("mv_y_q_scale_enc", "mv_y_q_scale_dec", "y_q_scale_enc", "y_q_scale_dec")}
         self._q_cache = {}
-        torch.cuda.synchronize(self.dev)
+        if strict:
+            ctx.check_strict([k for k in sd if k.startswith("bit_estimator") or "_q_" in k])
         return self
 
     def update(self, force=False):

@@ -71,12 +71,12 @@ def _t0():
     return e
 
 
-def _t1(e0, family, flops, nbytes):
+def _t1(e0, family, flops, nbytes, key=""):
     if e0 is None:
         return
     e = torch.cuda.Event(enable_timing=True)
     e.record()
-    PROFILE.append((family, e0, e, flops, nbytes))
+    PROFILE.append((family, e0, e, flops, nbytes, key))
 
 
 def _esz(dtype):
@@ -207,7 +207,8 @@ def conv(cw, x, y=None, *, out_dtype=None, in_op=IN_NONE, in_slope=0.0, act=ACT_
         flops = 2 * Ho * Wo * cw.cout * cw.cin * cw.kh * cw.kw
         nb = (x.H * x.W * x.C * _esz(x.dtype) + cw.w.numel() * cw.w.element_size()
               + y.H * y.W * y.C * _esz(y.dtype) * (1 + (res is not None) + (res2 is not None)))
-        _t1(e0, "conv", flops, nb)
+        _t1(e0, "conv", flops, nb, f"k{cw.kh}s{cw.stride} {cw.cin}->{cw.cout} {x.H}x{x.W} "
+            f"{'bf16' if cw.compute == BF16 else 'f32'} in{x.dtype}out{y.dtype}{' shuf' if shuffle else ''}")
     return y
 
 

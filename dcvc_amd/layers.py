@@ -42,20 +42,34 @@ class Ctx:
         self.sd = state_dict
         self.dev = device
         self.prec = prec
+        self.used = set()
 
     def has(self, name):
         return name + ".weight" in self.sd
 
+    def take(self, key):
+        if key not in self.sd:
+            raise KeyError(f"missing key in state_dict: {key}")
+        self.used.add(key)
+        return self.sd[key]
+
+    def check_strict(self, extra_used=()):
+        """load_state_dict(strict=True): every key must be consumed."""
+        unused = set(self.sd) - self.used - set(extra_used)
+        if unused:
+            raise RuntimeError(f"unexpected key(s) in state_dict: {sorted(unused)[:8]}")
+
     def conv(self, name, stride=1, latent=False, compute=None):
         if compute is None:
             compute = self.prec.latent_compute if latent else self.prec.feat_compute
-        return K.ConvW(self.sd[name + ".weight"], self.sd.get(name + ".bias"), stride, compute, self.dev)
+        b = self.take(name + ".bias") if name + ".bias" in self.sd else None
+        return K.ConvW(self.take(name + ".weight"), b, stride, compute, self.dev)
 
     def dw(self, name):
-        w = self.sd[name + ".weight"].detach().float().cpu()  # [C,1,3,3]
+        w = self.take(name + ".weight").detach().float().cpu()  # [C,1,3,3]
         C = w.shape[0]
         w9c = w.reshape(C, 9).t().contiguous().to(self.dev)  # [9][C]
-        b = self.sd[name + ".bias"].detach().float().contiguous().to(self.dev)
+        b = self.take(name + ".bias").detach().float().contiguous().to(self.dev)
         return w9c, b
 
     def dtype(self, latent):
@@ -248,7 +262,8 @@ def hyper_enc(ctx, p, reduce_enc_layer):
 
 def hyper_dec(ctx, p):
     """get_hyper_enc_dec_models decoder (video_net.py:239-249)."""
-    c0, c2, c4, c6, c8 = (ctx.conv(f"{p}.{i}", 1, True) for i in (0, 2, 4, 6, 8))
+    c0, c4, c8 = (ctx.conv(f"{p}.{i}", 1, True) for i in (0, 4, 8))
+    c2, c6 = (ctx.conv(f"{p}.{i}.0", 1, True) for i in (2, 6))  # subpel_conv1x1 = Sequential(conv, shuffle)
 
     def run(x, y=None):
         x = K.conv(c0, x, act=ACT_LRELU, slope=0.01)

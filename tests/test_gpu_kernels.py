@@ -53,7 +53,35 @@ CONV_CASES = [
     (64, 128, 2, 2, 8, 8),
     (96, 256, 3, 1, 7, 11),
     (1024, 384, 1, 1, 5, 6),
+    (64, 64, 3, 1, 70, 90),
+    (32, 128, 1, 1, 40, 64),
+    (128, 512, 1, 1, 33, 47),
+    (256, 768, 1, 1, 17, 30),
 ]
+
+
+@pytest.mark.parametrize("mode", ["f32", "bf16"])
+def test_conv_vector_paths_with_channel_views(mode):
+    """16-byte staging and 4-channel stores on views with aligned offsets."""
+    h = K()
+    comp = h.F32 if mode == "f32" else h.BF16
+    dt = h.F32 if mode == "f32" else h.BF16
+    cin, cout, H, W = 64, 48, 29, 37
+    big = torch.randn(1, cin + 16, H, W)
+    x = big[:, 8:8 + cin]
+    w = torch.randn(cout, cin, 3, 3) / (cin * 9) ** 0.5
+    b = torch.randn(cout) * 0.1
+    r = torch.randn(1, cout, H, W)
+    ref = F.leaky_relu(F.conv2d(x, w, b, padding=1), 0.1) + r
+    cw = h.ConvW(w, b, 1, comp)
+    xa = to_act(big, dt).ch(8, cin)
+    out = h.empty(H, W, cout + 8, dt)
+    ra = h.empty(H, W, cout + 4, dt)
+    h.copy(to_act(r, h.F32), ra.ch(4, cout))
+    h.conv(cw, xa, out.ch(8, cout), act=h.ACT_LRELU, slope=0.1, res=ra.ch(4, cout))
+    torch.cuda.synchronize()
+    tol = 2e-5 if mode == "f32" else 2e-2
+    assert rel_err(back(out.ch(8, cout)), ref) < tol
 
 
 @pytest.mark.parametrize("case", CONV_CASES)

@@ -24,7 +24,7 @@ pytestmark = pytest.mark.gpu
 
 # max fraction of symbols differing from the oracle, max |bits - oracle| / oracle,
 # max |PSNR - oracle PSNR| in dB (random-weight sequences, PSNR ~6-7 dB)
-PARITY_TOL = {"sym_frac": 2e-3, "bits_rel": 2e-3, "psnr_db": 2e-3}
+PARITY_TOL = {"sym_frac": 2e-3, "bits_rel": 5e-3, "psnr_db": 1e-4}
 FAST_TOL = {"sym_frac": 0.05, "bits_rel": 0.02, "psnr_db": 0.05}
 
 OUT = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "gpurun_out")
@@ -140,4 +140,14 @@ def test_fast_mode_vs_oracle(dc_golden, oracle_runs, tag):
     from dcvc_amd.layers import Precision
     stats = compare(run_product(dc_golden, tag, Precision.fast()), oracle_runs[tag])
     _dump(f"fast_{tag}", stats)
+    check(stats, FAST_TOL)
+
+
+@pytest.mark.parametrize("tag", ["B", "A"])
+def test_fast_bf16_latent_vs_oracle(dc_golden, oracle_runs, tag):
+    """bf16 MFMA for the entropy-parameter tail too (fp32 storage)."""
+    from dcvc_amd.layers import Precision
+    from dcvc_amd.hip import BF16
+    stats = compare(run_product(dc_golden, tag, Precision.fast(latent_compute=BF16)), oracle_runs[tag])
+    _dump(f"fast_bf16lat_{tag}", stats)
     check(stats, FAST_TOL)
