@@ -472,6 +472,8 @@ int pick_bn(const ConvP &p, hipStream_t st) {
   }
 }
 
+int g_use_gemm = 1;  // dcvc_set_option("gemm1x1", 0) routes 1x1 convs to the generic kernel
+
 bool valid_view(const dcvc_tensor &t) {
   return t.ptr && t.H > 0 && t.W > 0 && t.C > 0 && t.coff >= 0 && t.coff + t.C <= t.cstride &&
          (t.dtype == DCVC_F32 || t.dtype == DCVC_BF16);
@@ -504,6 +506,8 @@ extern "C" int64_t dcvc_conv_pack_weights(const float *w, int cout, int cin, int
         }
   return total;
 }
+
+extern "C" int dcvc_internal_gemm1x1(const dcvc_conv_args *a, void *stream);
 
 extern "C" int dcvc_conv2d(const dcvc_conv_args *a, void *stream) {
   if (!a || !a->w || !valid_view(a->x) || !valid_view(a->y)) return DCVC_HIP_EINVAL;
@@ -556,6 +560,10 @@ extern "C" int dcvc_conv2d(const dcvc_conv_args *a, void *stream) {
     p.r2cs = a->res2.cstride;
     p.r2co = a->res2.coff;
   }
+  if (a->kh == 1 && a->kw == 1 && a->stride == 1 && a->compute == DCVC_BF16 && g_use_gemm) {
+    const int r = dcvc_internal_gemm1x1(a, stream);
+    if (r != DCVC_HIP_EUNSUPPORTED) return r;
+  }
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const bool xin32 = a->x.dtype == DCVC_F32, yout32 = a->y.dtype == DCVC_F32;
   {
@@ -576,4 +584,13 @@ extern "C" int dcvc_conv2d(const dcvc_conv_args *a, void *stream) {
   if (xin32 && !yout32) return pick_bn<float, uint16_t, false>(p, st);
   if (!xin32 && yout32) return pick_bn<uint16_t, float, false>(p, st);
   return pick_bn<uint16_t, uint16_t, false>(p, st);
+}
+
+extern "C" int dcvc_set_option(const char *name, int value) {
+  if (!name) return DCVC_HIP_EINVAL;
+  if (std::strcmp(name, "gemm1x1") == 0) {
+    g_use_gemm = value;
+    return DCVC_HIP_OK;
+  }
+  return DCVC_HIP_EINVAL;
 }

@@ -40,6 +40,7 @@ _vp, _i, _f = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
 HIP_SYMBOLS = [
     ("dcvc_conv_pack_weights", ctypes.c_int64, [_vp, _i, _i, _i, _i, _i, _vp]),
     ("dcvc_conv2d", _i, [ctypes.POINTER(CConvArgs), _vp]),
+    ("dcvc_set_option", _i, [ctypes.c_char_p, _i]),
     ("dcvc_dwconv3x3", _i, [_T, _T, _vp, _vp, _vp]),
     ("dcvc_flow_warp", _i, [_T, _T, _T, _vp, _vp, _vp]),
     ("dcvc_offset_diversity", _i, [_T, _T, _T, _T, _vp, _vp, _vp, _vp, _f, _vp]),
@@ -88,6 +89,10 @@ def lib():
     if _L is None:
         _L = hip_lib()
     return _L
+
+
+def set_option(name, value):
+    check(lib().dcvc_set_option(name.encode(), int(value)), "set_option")
 
 
 def stream():

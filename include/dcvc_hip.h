@@ -90,6 +90,9 @@ typedef struct dcvc_conv_args {
 int64_t dcvc_conv_pack_weights(const float *w, int cout, int cin, int kh,
                                int kw, int compute, void *out);
 int dcvc_conv2d(const dcvc_conv_args *a, void *stream);
+/* Runtime switches (testing / A-B): "gemm1x1" = 1 (default) routes 1x1
+ * stride-1 bf16 convs to the double-buffered GEMM kernel. */
+int dcvc_set_option(const char *name, int value);
 
 /* Depthwise 3x3 conv, stride 1, padding 1, + bias (DepthConv.depth_conv,
  * DCVC-DC/src/models/layers.py:143-144).  w: [9][C] fp32 (tap-major). */

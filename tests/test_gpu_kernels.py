@@ -245,3 +245,35 @@ def test_quadtree_encode_decode_steps_match_oracle():
         ref_idx = O.build_indexes(sc_w[k], log_min, log_step).to(torch.int16).reshape(-1)
         assert (idx.cpu() != ref_idx).sum().item() <= 1
     assert torch.equal(back(yh), y_hat)
+
+
+@pytest.mark.parametrize("case", [(48, 192, 37, 61), (384, 384, 9, 13), (96, 48, 20, 33), (40, 64, 17, 19),
+                                  (1024, 384, 5, 6), (64, 256, 30, 40)])
+@pytest.mark.parametrize("xdt", ["f32", "bf16"])
+def test_gemm1x1_equals_generic_conv(case, xdt):
+    """The double-buffered 1x1 GEMM kernel and the generic conv kernel
+    accumulate the same 32-channel MFMA blocks in the same order: outputs are
+    bit-identical, including lrelu input op, residual, scale and shuffle."""
+    h = K()
+    cin, cout, H, W = case
+    dt = h.F32 if xdt == "f32" else h.BF16
+    x = torch.randn(1, cin, H, W)
+    w = torch.randn(cout, cin, 1, 1) / cin ** 0.5
+    b = torch.randn(cout) * 0.1
+    cw = h.ConvW(w, b, 1, h.BF16)
+    xa = to_act(x, dt)
+    outs = []
+    rt = torch.randn(1, cout, H, W)
+    for use in (1, 0):
+        h.set_option("gemm1x1", use)
+        r = h.empty(H, W, cout, h.BF16)
+        h.copy(to_act(rt, h.F32), r)
+        y = h.conv(cw, xa, out_dtype=h.BF16, in_op=h.IN_LRELU, in_slope=0.1, act=h.ACT_LRELU, slope=0.01, res=r)
+        y2 = h.conv(cw, xa, shuffle=cout % 4 == 0, out_dtype=h.F32) if cout % 4 == 0 else y
+        torch.cuda.synchronize()
+        outs.append((back(y), back(y2)))
+    h.set_option("gemm1x1", 1)
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert torch.equal(outs[0][1], outs[1][1])
+    ref = F.leaky_relu(F.conv2d(F.leaky_relu(x, 0.1), w, b), 0.01) + rt
+    assert rel_err(back(y), ref) < 2e-2
