@@ -23,7 +23,6 @@
 namespace {
 
 constexpr int kChunk = 32;  // input channels per K chunk
-__constant__ int kSwz[4] = {0, 2, 3, 1};
 
 struct ConvP {
   const void *x;
@@ -53,8 +52,10 @@ struct ConvP {
 
 // LDS image helpers ---------------------------------------------------------
 // bf16: a "row" is 32 channels = 64 B = 4 slots of 16 B; slot is swizzled.
+// slot XOR {0, 2, 3, 1}[(row >> 2) & 3], as a nibble table in a register
 __device__ __forceinline__ int swz_off_bf16(int row, int slot) {
-  return row * 32 + ((slot ^ kSwz[(row >> 2) & 3]) << 3);  // in bf16 elements
+  const int x = (0x1320 >> (((row >> 2) & 3) << 2)) & 3;
+  return row * 32 + ((slot ^ x) << 3);  // in bf16 elements
 }
 // f32: a row is 32 floats padded to 33.
 __device__ __forceinline__ int off_f32(int row, int k) { return row * 33 + k; }

@@ -145,14 +145,10 @@ __global__ void frame_kernel(const uint8_t *src, int h, int w, View y) {
 // ------------------------------------------------------------ quadtree prior
 // Step k processes, for each pixel with parity m = 2*(y&1) + (x&1), the
 // channel quarter q with STEP_MASK[k][q] == m (common_model.py:168-220).
-__constant__ int kStepMask[4][4] = {{0, 1, 2, 3}, {3, 2, 1, 0}, {2, 3, 0, 1}, {1, 0, 3, 2}};
-
+// STEP_MASK = {{0,1,2,3},{3,2,1,0},{2,3,0,1},{1,0,3,2}} is q -> q ^ {0,3,2,1}[k],
+// an involution, so the quarter of mask m at step k is m ^ {0,3,2,1}[k].
 __device__ __forceinline__ int quarter_of(int k, int m) {
-  int q = 0;
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-    if (kStepMask[k][i] == m) q = i;
-  return q;
+  return m ^ ((0x1230 >> (k << 2)) & 3);
 }
 
 __device__ __forceinline__ int16_t scale_index(float s, float log_min, float log_step) {

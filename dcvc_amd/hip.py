@@ -26,6 +26,18 @@ class CTensor(ctypes.Structure):
                 ("coff", ctypes.c_int)]
 
 
+class CDcbArgs(ctypes.Structure):
+    _fields_ = [("x", CTensor), ("y", CTensor), ("cin", ctypes.c_int), ("cout", ctypes.c_int),
+                ("gated", ctypes.c_int),
+                ("w_conv1", ctypes.c_void_p), ("ld_conv1", ctypes.c_int), ("b_conv1", ctypes.c_void_p),
+                ("w_dw", ctypes.c_void_p), ("b_dw", ctypes.c_void_p),
+                ("w_conv2", ctypes.c_void_p), ("ld_conv2", ctypes.c_int), ("b_conv2", ctypes.c_void_p),
+                ("w_adaptor", ctypes.c_void_p), ("ld_adaptor", ctypes.c_int), ("b_adaptor", ctypes.c_void_p),
+                ("w_ffn1", ctypes.c_void_p), ("ld_ffn1", ctypes.c_int), ("b_ffn1", ctypes.c_void_p),
+                ("w_ffn2", ctypes.c_void_p), ("ld_ffn2", ctypes.c_int), ("b_ffn2", ctypes.c_void_p),
+                ("scale", ctypes.c_void_p), ("slope_dc", ctypes.c_float), ("slope_ffn", ctypes.c_float)]
+
+
 class CConvArgs(ctypes.Structure):
     _fields_ = [("x", CTensor), ("y", CTensor), ("w", ctypes.c_void_p), ("bias", ctypes.c_void_p),
                 ("cin", ctypes.c_int), ("cout", ctypes.c_int), ("kh", ctypes.c_int), ("kw", ctypes.c_int),
@@ -41,6 +53,7 @@ HIP_SYMBOLS = [
     ("dcvc_conv_pack_weights", ctypes.c_int64, [_vp, _i, _i, _i, _i, _i, _vp]),
     ("dcvc_conv2d", _i, [ctypes.POINTER(CConvArgs), _vp]),
     ("dcvc_set_option", _i, [ctypes.c_char_p, _i]),
+    ("dcvc_depthconv_block", _i, [ctypes.POINTER(CDcbArgs), _vp]),
     ("dcvc_dwconv3x3", _i, [_T, _T, _vp, _vp, _vp]),
     ("dcvc_flow_warp", _i, [_T, _T, _T, _vp, _vp, _vp]),
     ("dcvc_offset_diversity", _i, [_T, _T, _T, _T, _vp, _vp, _vp, _vp, _f, _vp]),
@@ -214,6 +227,39 @@ def conv(cw, x, y=None, *, out_dtype=None, in_op=IN_NONE, in_slope=0.0, act=ACT_
               + y.H * y.W * y.C * _esz(y.dtype) * (1 + (res is not None) + (res2 is not None)))
         _t1(e0, "conv", flops, nb, f"k{cw.kh}s{cw.stride} {cw.cin}->{cw.cout} {x.H}x{x.W} "
             f"{'bf16' if cw.compute == BF16 else 'f32'} in{x.dtype}out{y.dtype}{' shuf' if shuffle else ''}")
+    return y
+
+
+UNSUPPORTED = -3
+
+
+def depthconv_block(blk, x, y, scale=None):
+    """Fused DepthConvBlock(2) (dcvc_depthconv_block).  Returns y, or None when
+    no fused kernel is instantiated for this shape (caller runs unfused)."""
+    a = CDcbArgs()
+    a.x, a.y = x.c(), y.c()
+    a.cin, a.cout, a.gated = blk.conv1.cin, blk.ffn2.cout, 1 if blk.gated else 0
+    cp = lambda cw: (cw.w.data_ptr(), cw.w.numel() // cw.cout, cw.b.data_ptr())  # noqa: E731
+    a.w_conv1, a.ld_conv1, a.b_conv1 = cp(blk.conv1)
+    a.w_dw, a.b_dw = blk.dw[0].data_ptr(), blk.dw[1].data_ptr()
+    a.w_conv2, a.ld_conv2, a.b_conv2 = cp(blk.conv2)
+    if blk.adaptor is not None:
+        a.w_adaptor, a.ld_adaptor, a.b_adaptor = cp(blk.adaptor)
+    a.w_ffn1, a.ld_ffn1, a.b_ffn1 = cp(blk.ffn1)
+    a.w_ffn2, a.ld_ffn2, a.b_ffn2 = cp(blk.ffn2)
+    a.scale = scale.data_ptr() if scale is not None else None
+    a.slope_dc, a.slope_ffn = blk.slope_dc, blk.slope_ffn
+    e0 = _t0()
+    r = lib().dcvc_depthconv_block(ctypes.byref(a), stream())
+    if r == UNSUPPORTED:
+        return None
+    check(r, "depthconv_block")
+    if e0 is not None:
+        hid = 2 * a.cout if blk.gated else max(min(4 * a.cout, 1024), 2 * a.cout)
+        n = x.H * x.W
+        fl = 2 * n * (a.cin * a.cin + 9 * a.cin + a.cin * a.cout * (2 if blk.adaptor is not None else 1)
+                      + a.cout * hid * (3 if blk.gated else 2))
+        _t1(e0, "dcb_fused", fl, n * (a.cin + a.cout) * 2, f"dcb {a.cin}->{a.cout} {x.H}x{x.W}")
     return y
 
 

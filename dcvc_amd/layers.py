@@ -19,6 +19,9 @@ from . import hip as K
 from .hip import Act, F32, BF16, ACT_LRELU, ACT_NONE, IN_LRELU, IN_GATE
 
 
+FUSE_DCB = True   # fused DepthConvBlock kernel where instantiated (A/B switch)
+
+
 class Precision:
     def __init__(self, feat, feat_compute, latent_compute):
         self.feat = feat
@@ -114,6 +117,11 @@ class DepthConvBlock:
     def __call__(self, x, y=None, scale=None):
         ctx = self.ctx
         dt = ctx.dtype(self.latent)
+        if (FUSE_DCB and not self.latent and x.dtype == BF16 and dt == BF16
+                and self.conv1.compute == BF16 and self.cout <= 128 and x.C <= 128):
+            out = y if y is not None else K.empty(x.H, x.W, self.cout, BF16, x.buf.device)
+            if K.depthconv_block(self, x, out, scale) is not None:
+                return out
         x = ctx.fit(x, self.conv1.compute)
         if self.adaptor is not None:
             idn = K.conv(self.adaptor, x, out_dtype=dt)

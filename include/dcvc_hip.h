@@ -94,6 +94,29 @@ int dcvc_conv2d(const dcvc_conv_args *a, void *stream);
  * stride-1 bf16 convs to the double-buffered GEMM kernel. */
 int dcvc_set_option(const char *name, int value);
 
+/*
+ * Fused DepthConvBlock (DepthConv + ConvFFN) / DepthConvBlock2 (+ ConvFFN2),
+ * DCVC-DC/src/models/layers.py:135-222, for bf16 feature maps with
+ * Cin, Cout <= 128: one kernel, all intermediates in LDS.  Weights are the
+ * packed bf16 1x1 layouts of dcvc_conv_pack_weights ([N][ld], ld = K rounded
+ * up to 32); the depthwise weights are [9][Cin] fp32.  w_adaptor NULL means
+ * identity (Cin == Cout).  Returns DCVC_HIP_EUNSUPPORTED for shapes without
+ * an instantiated kernel (the caller then runs the unfused sequence).
+ */
+typedef struct dcvc_dcb_args {
+  dcvc_tensor x, y;
+  int cin, cout, gated;
+  const void *w_conv1; int ld_conv1; const float *b_conv1;
+  const float *w_dw; const float *b_dw;
+  const void *w_conv2; int ld_conv2; const float *b_conv2;
+  const void *w_adaptor; int ld_adaptor; const float *b_adaptor;
+  const void *w_ffn1; int ld_ffn1; const float *b_ffn1;
+  const void *w_ffn2; int ld_ffn2; const float *b_ffn2;
+  const float *scale;
+  float slope_dc, slope_ffn;
+} dcvc_dcb_args;
+int dcvc_depthconv_block(const dcvc_dcb_args *a, void *stream);
+
 /* Depthwise 3x3 conv, stride 1, padding 1, + bias (DepthConv.depth_conv,
  * DCVC-DC/src/models/layers.py:143-144).  w: [9][C] fp32 (tap-major). */
 int dcvc_dwconv3x3(dcvc_tensor x, dcvc_tensor y, const float *w,

@@ -277,3 +277,54 @@ def test_gemm1x1_equals_generic_conv(case, xdt):
     assert torch.equal(outs[0][1], outs[1][1])
     ref = F.leaky_relu(F.conv2d(F.leaky_relu(x, 0.1), w, b), 0.01) + rt
     assert rel_err(back(y), ref) < 2e-2
+
+
+DCB_SHAPES = [(48, 32, False), (32, 64, False), (64, 128, False), (128, 128, False), (128, 64, False),
+              (64, 48, False), (64, 64, False), (16, 32, True), (32, 64, True), (64, 128, True),
+              (128, 128, True), (128, 64, True), (64, 16, True)]
+
+
+def _dcb_state(cin, cout, gated, seed):
+    from dcvc_amd.weights import synthetic_state_dict
+    p = "b.block"
+    spec = [(f"{p}.0.conv1.0.weight", (cin, cin, 1, 1)), (f"{p}.0.conv1.0.bias", (cin,)),
+            (f"{p}.0.depth_conv.weight", (cin, 1, 3, 3)), (f"{p}.0.depth_conv.bias", (cin,)),
+            (f"{p}.0.conv2.weight", (cout, cin, 1, 1)), (f"{p}.0.conv2.bias", (cout,))]
+    if cin != cout:
+        spec += [(f"{p}.0.adaptor.weight", (cout, cin, 1, 1)), (f"{p}.0.adaptor.bias", (cout,))]
+    if gated:
+        spec += [(f"{p}.1.conv.weight", (4 * cout, cout, 1, 1)), (f"{p}.1.conv.bias", (4 * cout,)),
+                 (f"{p}.1.conv_out.weight", (cout, 2 * cout, 1, 1)), (f"{p}.1.conv_out.bias", (cout,))]
+    else:
+        hid = max(min(4 * cout, 1024), 2 * cout)
+        spec += [(f"{p}.1.conv.0.weight", (hid, cout, 1, 1)), (f"{p}.1.conv.0.bias", (hid,)),
+                 (f"{p}.1.conv.2.weight", (cout, hid, 1, 1)), (f"{p}.1.conv.2.bias", (cout,))]
+    return synthetic_state_dict(spec, seed=seed, gain=1.5)
+
+
+@pytest.mark.parametrize("shape", DCB_SHAPES)
+def test_fused_depthconv_block_matches_unfused(shape):
+    """The fused DepthConvBlock kernel reproduces the unfused bf16 kernel
+    sequence (same roundings, same accumulation order) and the fp32 oracle."""
+    from dcvc_amd import layers as L
+    from oracle import dc_oracle as O
+    h = K()
+    cin, cout, gated = shape
+    sd = _dcb_state(cin, cout, gated, seed=cin * 7 + cout)
+    ctx = L.Ctx(sd, torch.device("cuda"), L.Precision.fast())
+    blk = L.DepthConvBlock(ctx, "b", gated=gated)
+    H, W = 37, 45
+    x = torch.randn(1, cin, H, W)
+    xa = to_act(x, h.BF16)
+    sc = torch.rand(cout) + 0.5
+    outs = []
+    for fuse in (True, False):
+        L.FUSE_DCB = fuse
+        outs.append(back(blk(xa, scale=sc.cuda())))
+    L.FUSE_DCB = True
+    torch.cuda.synchronize()
+    diff = (outs[0] - outs[1]).abs().max().item()
+    assert diff <= 1e-2 * outs[1].abs().max().item(), diff
+    fn = O.depth_conv_block2 if gated else O.depth_conv_block
+    ref = fn(O.Params(sd), "b", x.to(torch.bfloat16).float()) * sc.view(1, -1, 1, 1)
+    assert rel_err(outs[0], ref) < 3e-2
