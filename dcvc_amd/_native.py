@@ -102,7 +102,9 @@ def hip_lib():
     global _hip
     if _hip is None:
         from .hip import HIP_SYMBOLS
-        _hip = _bind(_load("libdcvc_hip.so"), HIP_SYMBOLS)
+        # DCVC_HIP_LIB names an alternative build in dcvc_amd/lib (kernel
+        # A/B experiments, scripts/conv_microbench.py); default is the product.
+        _hip = _bind(_load(os.environ.get("DCVC_HIP_LIB", "libdcvc_hip.so")), HIP_SYMBOLS)
     return _hip
 
 

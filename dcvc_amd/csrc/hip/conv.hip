@@ -17,6 +17,7 @@
 // a per-channel scale and pixel-shuffle, in the order the reference applies
 // them (see dcvc_conv_args in include/dcvc_hip.h).
 #include "common.h"
+#include "epilogue.h"
 
 #include <cstring>
 
@@ -46,7 +47,8 @@ struct ConvP {
   int Wout;  // width of y buffer (after shuffle)
   int tiles_x, tiles_y;
   int vec;      // 16-byte input staging allowed (channel alignment)
-  int vec_out;  // 4-channel vector epilogue allowed (no shuffle, alignment)
+  int vec_out;  // 8-channel vector epilogue allowed (alignment)
+  int lc_off;   // LDS byte offset of the epilogue constants (bias, scale)
   int wall;     // stage all kernel rows' weights per chunk
 };
 
@@ -98,8 +100,12 @@ __device__ __forceinline__ void stage_input(const ConvP &p, void *lds_in, int ch
                                             int IWp) {
   const int items = IH * IW * 4;
   const TIN *X = reinterpret_cast<const TIN *>(p.x);
+  // bf16 -> bf16 with no input transform: move the raw 16-byte pieces
+  constexpr bool kRawOk = !F32 && sizeof(TIN) == 2;
+  const bool raw = kRawOk && p.vec && p.in_op == DCVC_IN_NONE;
   for (int base = threadIdx.x; base < items; base += 256 * kU) {
     float v[kU][8];
+    u16x8 rv[kU];
     int rows[kU];
 #pragma unroll
     for (int u = 0; u < kU; ++u) {
@@ -113,6 +119,18 @@ __device__ __forceinline__ void stage_input(const ConvP &p, void *lds_in, int ch
       const int c0 = ch0 + slot * 8;
       rows[u] = (iy * IWp + ix) * 4 + slot;
       const bool inb = gy >= 0 && gy < p.H && gx >= 0 && gx < p.W && c0 < p.cin;
+      if constexpr (kRawOk) {
+        if (raw) {
+          const int64_t e = ((int64_t)gy * p.W + gx) * p.xcs + p.xco + c0;
+          if (inb) {
+            rv[u] = *reinterpret_cast<const u16x8 *>(reinterpret_cast<const uint16_t *>(X) + e);
+          } else {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) rv[u][j] = 0;
+          }
+          continue;
+        }
+      }
       if (p.vec) {
         if (inb) {
           const int64_t e = ((int64_t)gy * p.W + gx) * p.xcs + p.xco + c0;
@@ -138,11 +156,17 @@ __device__ __forceinline__ void stage_input(const ConvP &p, void *lds_in, int ch
 #pragma unroll
     for (int u = 0; u < kU; ++u) {
       if (rows[u] < 0) continue;
+      const int row = rows[u] >> 2, slot = rows[u] & 3;
+      if constexpr (kRawOk) {
+        if (raw) {
+          *reinterpret_cast<u16x8 *>(reinterpret_cast<uint16_t *>(lds_in) + swz_off_bf16(row, slot)) = rv[u];
+          continue;
+        }
+      }
       if (p.vec && p.in_op == DCVC_IN_LRELU) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[u][j] = v[u][j] >= 0.f ? v[u][j] : v[u][j] * p.in_slope;
       }
-      const int row = rows[u] >> 2, slot = rows[u] & 3;
       if constexpr (F32) {
         float *L = reinterpret_cast<float *>(lds_in);
 #pragma unroll
@@ -225,32 +249,6 @@ __device__ __forceinline__ void stage_weights(const ConvP &p, void *lds_w, int n
   }
 }
 
-template <typename TOUT>
-__device__ __forceinline__ void store4(const ConvP &p, int64_t pix, int c, const float v[4]);
-template <>
-__device__ __forceinline__ void store4<float>(const ConvP &p, int64_t pix, int c, const float v[4]) {
-  *reinterpret_cast<float4 *>(reinterpret_cast<float *>(p.y) + pix * p.ycs + p.yco + c) =
-      make_float4(v[0], v[1], v[2], v[3]);
-}
-template <>
-__device__ __forceinline__ void store4<uint16_t>(const ConvP &p, int64_t pix, int c, const float v[4]) {
-  u16x4 o;
-  o[0] = f2bf(v[0]); o[1] = f2bf(v[1]); o[2] = f2bf(v[2]); o[3] = f2bf(v[3]);
-  *reinterpret_cast<u16x4 *>(reinterpret_cast<uint16_t *>(p.y) + pix * p.ycs + p.yco + c) = o;
-}
-template <typename T>
-__device__ __forceinline__ void load4(const void *base, int64_t e, float v[4]);
-template <>
-__device__ __forceinline__ void load4<float>(const void *base, int64_t e, float v[4]) {
-  const float4 a = *reinterpret_cast<const float4 *>(reinterpret_cast<const float *>(base) + e);
-  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
-}
-template <>
-__device__ __forceinline__ void load4<uint16_t>(const void *base, int64_t e, float v[4]) {
-  const u16x4 a = *reinterpret_cast<const u16x4 *>(reinterpret_cast<const uint16_t *>(base) + e);
-  v[0] = bf2f(a[0]); v[1] = bf2f(a[1]); v[2] = bf2f(a[2]); v[3] = bf2f(a[3]);
-}
-
 template <typename TIN, typename TOUT, bool F32, int BN, int TH>
 __global__ void __launch_bounds__(256) conv_kernel(ConvP p) {
   constexpr int RW = TH / 4;   // output rows per wave
@@ -273,6 +271,8 @@ __global__ void __launch_bounds__(256) conv_kernel(ConvP p) {
   const int in_elems = IH * IWp * (F32 ? 33 : 32);
   void *lds_in = smem;
   void *lds_w = smem + ((in_elems * (F32 ? 4 : 2) + 15) & ~15);
+  float *Lc = reinterpret_cast<float *>(smem + p.lc_off);
+  epi::stage_consts(p, Lc, n0, BN);  // published by the chunk loop's first barrier
 
   f32x4 acc[RW][NT];
 #pragma unroll
@@ -337,65 +337,22 @@ __global__ void __launch_bounds__(256) conv_kernel(ConvP p) {
     }
   }
 
-  // ---- epilogue: lane owns pixel (oy, ox) and channels n..n+3 per tile
-  const int ox = ox0 + col;
-  if (ox >= p.Wo) return;
+  // ---- epilogue (epilogue.h): fp32 tile in LDS, then coalesced stores
+  __syncthreads();
+  float *T = reinterpret_cast<float *>(smem);
+  constexpr int LD = BN + 4;
 #pragma unroll
-  for (int r = 0; r < RW; ++r) {
-    const int oy = oy0 + wave * RW + r;
-    if (oy >= p.Ho) continue;
+  for (int r = 0; r < RW; ++r)
 #pragma unroll
-    for (int j = 0; j < NT; ++j) {
-      const int nb = n0 + j * 16 + hi * 4;
-      if (nb >= p.cout) continue;
-      float v[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int n = nb + i;
-        float t = acc[r][j][i];
-        if (p.bias && n < p.cout) t += p.bias[n];
-        v[i] = apply_act(p.act, t, p.slope);
-      }
-      if (p.vec_out && nb + 3 < p.cout) {
-        const int64_t pix = (int64_t)oy * p.Wout + ox;
-        if (p.res) {
-          float rv[4];
-          load4<TOUT>(p.res, pix * p.rcs + p.rco + nb, rv);
-#pragma unroll
-          for (int i = 0; i < 4; ++i) v[i] = rv[i] + v[i];
-        }
-        if (p.res2) {
-          float rv[4];
-          load4<TOUT>(p.res2, pix * p.r2cs + p.r2co + nb, rv);
-#pragma unroll
-          for (int i = 0; i < 4; ++i) v[i] = rv[i] + v[i];
-        }
-        if (p.scale) {
-#pragma unroll
-          for (int i = 0; i < 4; ++i) v[i] = v[i] * p.scale[nb + i];
-        }
-        store4<TOUT>(p, pix, nb, v);
-        continue;
-      }
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int n = nb + i;
-        if (n >= p.cout) continue;
-        float t = v[i];
-        int c = n, yy = oy, xx = ox;
-        if (p.shuffle) {
-          c = n >> 2;
-          yy = oy * 2 + ((n >> 1) & 1);
-          xx = ox * 2 + (n & 1);
-        }
-        const int64_t pix = (int64_t)yy * p.Wout + xx;
-        if (p.res) t = ld<TOUT>(p.res, pix * p.rcs + p.rco + c) + t;
-        if (p.res2) t = ld<TOUT>(p.res2, pix * p.r2cs + p.r2co + c) + t;
-        if (p.scale) t = t * p.scale[c];
-        st<TOUT>(p.y, pix * p.ycs + p.yco + c, t);
-      }
-    }
-  }
+    for (int j = 0; j < NT; ++j)
+      epi::put4(p, T, LD, (wave * RW + r) * 16 + col, j * 16 + hi * 4, Lc, acc[r][j]);
+  __syncthreads();
+  epi::store_tile<TOUT, epi::ipt(TH * 16, BN, 256)>(p, T, LD, TH * 16, n0, min(BN, p.cout - n0), Lc, BN,
+                                                     [&](int l, int &oy, int &ox) {
+    oy = oy0 + (l >> 4);
+    ox = ox0 + (l & 15);
+    return oy < p.Ho && ox < p.Wo;
+  });
 }
 
 template <bool F32, int BN, int TH>
@@ -406,7 +363,9 @@ size_t lds_bytes(const ConvP &p, bool wall) {
   const size_t row = F32 ? 33 * 4 : 32 * 2;
   const size_t in_bytes = (size_t)IH * IWp * row;
   const size_t w_bytes = (size_t)(wall ? p.kh : 1) * p.kw * BN * row;
-  return ((in_bytes + 15) & ~(size_t)15) + w_bytes;
+  const size_t stage = ((in_bytes + 15) & ~(size_t)15) + w_bytes;
+  const size_t epi = (size_t)TH * 16 * (BN + 4) * 4;  // fp32 output tile
+  return stage > epi ? stage : epi;
 }
 
 template <typename TIN, typename TOUT, bool F32, int BN, int TH>
@@ -417,7 +376,8 @@ int launch(const ConvP &p0, hipStream_t st) {
   const int tiles_n = (p.cout + BN - 1) / BN;
   // stage every kernel row's weights at once when that keeps LDS modest
   p.wall = lds_bytes<F32, BN, TH>(p, true) <= 64 * 1024 ? 1 : 0;
-  const size_t lds = lds_bytes<F32, BN, TH>(p, p.wall);
+  p.lc_off = (int)((lds_bytes<F32, BN, TH>(p, p.wall) + 15) & ~(size_t)15);
+  const size_t lds = p.lc_off + epi::consts_floats(BN) * 4;
   if (lds > 160 * 1024) return DCVC_HIP_EUNSUPPORTED;
   const int64_t blocks = (int64_t)p.tiles_x * p.tiles_y * tiles_n;
   if (blocks <= 0) return DCVC_HIP_OK;
@@ -473,7 +433,8 @@ int pick_bn(const ConvP &p, hipStream_t st) {
   }
 }
 
-int g_use_gemm = 1;  // dcvc_set_option("gemm1x1", 0) routes 1x1 convs to the generic kernel
+int g_use_gemm = 1;   // dcvc_set_option("gemm1x1", 0) routes 1x1 convs to the generic kernel
+int g_use_conv3 = 1;  // dcvc_set_option("conv3x3", 0) routes 3x3 s1 convs to the generic kernel
 
 bool valid_view(const dcvc_tensor &t) {
   return t.ptr && t.H > 0 && t.W > 0 && t.C > 0 && t.coff >= 0 && t.coff + t.C <= t.cstride &&
@@ -509,6 +470,8 @@ extern "C" int64_t dcvc_conv_pack_weights(const float *w, int cout, int cin, int
 }
 
 extern "C" int dcvc_internal_gemm1x1(const dcvc_conv_args *a, void *stream);
+extern "C" int dcvc_internal_conv3x3(const dcvc_conv_args *a, void *stream);
+extern "C" void dcvc_internal_conv3x3_resident(int v);
 
 extern "C" int dcvc_conv2d(const dcvc_conv_args *a, void *stream) {
   if (!a || !a->w || !valid_view(a->x) || !valid_view(a->y)) return DCVC_HIP_EINVAL;
@@ -561,6 +524,10 @@ extern "C" int dcvc_conv2d(const dcvc_conv_args *a, void *stream) {
     p.r2cs = a->res2.cstride;
     p.r2co = a->res2.coff;
   }
+  if (a->kh == 3 && a->kw == 3 && a->stride == 1 && a->compute == DCVC_BF16 && g_use_conv3) {
+    const int r = dcvc_internal_conv3x3(a, stream);
+    if (r != DCVC_HIP_EUNSUPPORTED) return r;
+  }
   if (a->kh == 1 && a->kw == 1 && a->stride == 1 && a->compute == DCVC_BF16 && g_use_gemm) {
     const int r = dcvc_internal_gemm1x1(a, stream);
     if (r != DCVC_HIP_EUNSUPPORTED) return r;
@@ -571,10 +538,10 @@ extern "C" int dcvc_conv2d(const dcvc_conv_args *a, void *stream) {
     const int xa = xin32 ? 4 : 8;   // elements per 16 bytes
     p.vec = (a->cin % 8 == 0) && (p.xcs % xa == 0) && (p.xco % xa == 0) &&
             ((uintptr_t)p.x % 16 == 0);
-    const int ya = yout32 ? 4 : 4;  // 4 channels per vector store
-    bool vo = !a->shuffle && (p.ycs % ya == 0) && (p.yco % ya == 0) && ((uintptr_t)p.y % 16 == 0);
-    if (a->res.ptr) vo = vo && (p.rcs % 4 == 0) && (p.rco % 4 == 0);
-    if (a->res2.ptr) vo = vo && (p.r2cs % 4 == 0) && (p.r2co % 4 == 0);
+    // 8-channel (16/32-byte) pieces in the epilogue
+    bool vo = (p.ycs % 8 == 0) && (p.yco % 8 == 0) && ((uintptr_t)p.y % 16 == 0);
+    if (a->res.ptr) vo = vo && (p.rcs % 8 == 0) && (p.rco % 8 == 0) && ((uintptr_t)p.res % 16 == 0);
+    if (a->res2.ptr) vo = vo && (p.r2cs % 8 == 0) && (p.r2co % 8 == 0) && ((uintptr_t)p.res2 % 16 == 0);
     p.vec_out = vo ? 1 : 0;
   }
   if (a->compute == DCVC_F32) {
@@ -591,6 +558,14 @@ extern "C" int dcvc_set_option(const char *name, int value) {
   if (!name) return DCVC_HIP_EINVAL;
   if (std::strcmp(name, "gemm1x1") == 0) {
     g_use_gemm = value;
+    return DCVC_HIP_OK;
+  }
+  if (std::strcmp(name, "conv3x3") == 0) {
+    g_use_conv3 = value;
+    return DCVC_HIP_OK;
+  }
+  if (std::strcmp(name, "conv3x3_resident") == 0) {
+    dcvc_internal_conv3x3_resident(value);
     return DCVC_HIP_OK;
   }
   return DCVC_HIP_EINVAL;

@@ -1,0 +1,720 @@
+// 3x3 stride-1 convolution on bf16 NHWC maps: the dominant layer type of the
+// DCVC-DC feature / context / recon stacks.
+//
+// Same implicit GEMM as conv.hip (D[n][pixel] = W[n][k] X[k][pixel] on
+// v_mfma_f32_16x16x32_bf16, lane = 4 consecutive output channels of one
+// pixel) but with the geometry fixed at compile time so the inner loop is
+// nothing but LDS reads with immediate offsets and MFMAs:
+//   * workgroup = 4 waves, output tile TH rows x 16 columns x BN channels;
+//     the (TH+2) x 18 halo tile of one 32-channel chunk sits in LDS with a
+//     row pitch of 20 pixels;
+//   * the 16-byte slot of a pixel row is XORed with 2 * ((x >> 2) & 1),
+//     x = column in the tile: for any tap shift dx the 16 lanes of a
+//     ds_read_b128 group hit 16 distinct bank groups, and the swizzle of
+//     (row + dy * pitch) equals that of row, so every (dy, row) offset is a
+//     compile-time immediate off three per-lane bases (one per dx);
+//   * weights of a chunk are staged as [tap][n][32] with the same swizzle
+//     keyed by row (all 9 taps at once, or one kernel row at a time when
+//     BN >= 96 to keep LDS under 64 KB);
+//   * when Cin % 32 == 16 the last chunk holds 16 channels and one MFMA
+//     covers two taps (k = [tap 2p: 16 ch | tap 2p+1: 16 ch]), so 48- and
+//     80-channel layers waste no MFMA work on zero padding;
+//   * every thread's staging addresses are computed once per workgroup;
+//     bf16 pieces move as raw 16-byte words (lrelu input transform applied
+//     on the fly when requested);
+//   * the epilogue is epilogue.h's coalesced one.
+// For Cin % 32 == 0 the K sum runs in conv.hip's order (chunk, tap, 32
+// channels per MFMA), so results are bit-identical to it; with a 16-channel
+// tail chunk the tail's products are grouped two taps per MFMA, which moves
+// fp32 rounding only (tests/test_gpu_kernels.py checks both).
+#include "common.h"
+#include "epilogue.h"
+
+namespace {
+
+constexpr int kPitch = 20;  // LDS pixels per halo row (18 used)
+
+struct C3 {
+  const uint16_t *x;
+  int H, W, xcs, xco;
+  const uint16_t *w;  // packed [cout][3][3][cinp] bf16
+  int cinp;
+  const float *bias;
+  void *y;
+  int ycs, yco;
+  int cin, cout;
+  int in_op;
+  float in_slope;
+  int act;
+  float slope;
+  int shuffle;
+  const float *scale;
+  const void *res;
+  int rcs, rco;
+  const void *res2;
+  int r2cs, r2co;
+  int Wout, Ho, Wo;
+  int vec_out;
+  int tiles_x, tiles_y;
+  int nblk_n;  // resident-weight kernel: n-blocks (workgroup b serves n-block b % nblk_n)
+  int lc_off;  // per-workgroup kernel: LDS byte offset of the epilogue constants
+  int xbytes;  // bytes of x's buffer from p.x (LDS-DMA range check)
+};
+
+// element offset of 16-byte slot `slot` of LDS row `row` whose swizzle key is x
+__device__ __forceinline__ int swz(int row, int x, int slot) {
+  return row * 32 + ((slot ^ (((x >> 2) & 1) << 1)) << 3);
+}
+
+__device__ __forceinline__ void zero8(u16x8 &v) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = 0;
+}
+
+// Stage weight rows [row0, row0 + nrows) of chunk `ch` into Lw.  mode 0: row
+// (t, n) = taps t of a 32-channel chunk; mode 1 (tail): row (pair, n) =
+// [tap 2 pair | tap 2 pair + 1] x 16 channels.  tap0: first tap of row 0.
+template <int BN>
+__device__ __forceinline__ void stage_w(const C3 &p, uint16_t *Lw, int n0, int ch, int tap0, int ntaps,
+                                        bool tail) {
+  const int items = ntaps * BN * 4;
+  constexpr int kB = 4;
+  for (int base = threadIdx.x; base < items; base += 256 * kB) {
+    u16x8 v[kB];
+#pragma unroll
+    for (int u = 0; u < kB; ++u) {
+      const int it = base + u * 256;
+      zero8(v[u]);
+      if (it >= items) continue;
+      const int row = it >> 2, s = it & 3;
+      const int t = row / BN, n = n0 + row - t * BN;
+      if (n >= p.cout) continue;
+      int tap, c;
+      if (tail) {
+        tap = 2 * (tap0 + t) + (s >> 1);
+        c = ch * 32 + (s & 1) * 8;
+      } else {
+        tap = tap0 + t;
+        c = ch * 32 + s * 8;
+      }
+      if (tap < 9) v[u] = *reinterpret_cast<const u16x8 *>(p.w + ((int64_t)n * 9 + tap) * p.cinp + c);
+    }
+#pragma unroll
+    for (int u = 0; u < kB; ++u) {
+      const int it = base + u * 256;
+      if (it >= items) continue;
+      const int row = it >> 2;
+      *reinterpret_cast<u16x8 *>(Lw + swz(row, row, it & 3)) = v[u];
+    }
+  }
+}
+
+template <int BN, int TH, bool WSPLIT, typename TOUT>
+__global__ void __launch_bounds__(256) conv3x3_kernel(C3 p) {
+  constexpr int RW = TH / 4;              // output rows per wave
+  constexpr int NT = BN / 16;             // n tiles per wave
+  constexpr int IH = TH + 2;
+  constexpr int NPC = IH * 18 * 4;        // 16-byte input pieces per chunk
+  constexpr int PU = (NPC + 255) / 256;   // per thread
+  constexpr int ROWB = kPitch * 32;       // elements per halo row
+  extern __shared__ __align__(16) unsigned char smem[];
+  uint16_t *Li = reinterpret_cast<uint16_t *>(smem);
+  uint16_t *Lw = Li + IH * ROWB;
+  float *Lc = reinterpret_cast<float *>(smem + p.lc_off);
+
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int col = lane & 15, hi = lane >> 4;
+  int b = blockIdx.x;
+  const int tx = b % p.tiles_x;
+  b /= p.tiles_x;
+  const int ty = b % p.tiles_y;
+  const int tn = b / p.tiles_y;
+  const int ox0 = tx * 16, oy0 = ty * TH, n0 = tn * BN;
+  epi::stage_consts(p, Lc, n0, BN);  // published by the chunk loop's first barrier
+
+  // ---- per-thread staging plan (fixed for the workgroup)
+  const int slot = threadIdx.x & 3;
+  int gofs[PU], lofs[PU];
+#pragma unroll
+  for (int u = 0; u < PU; ++u) {
+    const int it = threadIdx.x + 256 * u;
+    lofs[u] = -1;
+    gofs[u] = -1;
+    if (it < NPC) {
+      const int pix = it >> 2;
+      const int iy = pix / 18, ix = pix - iy * 18;
+      const int gy = oy0 - 1 + iy, gx = ox0 - 1 + ix;
+      lofs[u] = swz(iy * kPitch + ix, ix, slot);
+      if (gy >= 0 && gy < p.H && gx >= 0 && gx < p.W) gofs[u] = (gy * p.W + gx) * p.xcs + p.xco + slot * 8;
+    }
+  }
+  // ---- per-lane MFMA operand bases
+  int offB[3];
+#pragma unroll
+  for (int dx = 0; dx < 3; ++dx) offB[dx] = swz(wave * RW * kPitch + col + dx, col + dx, hi);
+  const int offA = swz(col, col, hi);
+
+  f32x4 acc[RW][NT];
+#pragma unroll
+  for (int r = 0; r < RW; ++r)
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc[r][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nch = (p.cin + 31) >> 5;
+  const bool has_tail = (p.cin & 31) == 16;
+  const bool lrelu_in = p.in_op == DCVC_IN_LRELU;
+
+  for (int ch = 0; ch < nch; ++ch) {
+    const bool tail = has_tail && ch == nch - 1;
+    __syncthreads();
+    // input chunk -> Li (a tail chunk moves only slots 0, 1)
+    {
+      u16x8 v[PU];
+#pragma unroll
+      for (int u = 0; u < PU; ++u) {
+        zero8(v[u]);
+        if (gofs[u] >= 0 && !(tail && slot >= 2))
+          v[u] = *reinterpret_cast<const u16x8 *>(p.x + gofs[u] + ch * 32);
+      }
+#pragma unroll
+      for (int u = 0; u < PU; ++u) {
+        if (lofs[u] < 0 || (tail && slot >= 2)) continue;
+        if (lrelu_in) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const float f = bf2f(v[u][j]);
+            v[u][j] = f2bf(f >= 0.f ? f : f * p.in_slope);
+          }
+        }
+        *reinterpret_cast<u16x8 *>(Li + lofs[u]) = v[u];
+      }
+    }
+    if (tail) {
+      // 5 tap pairs; pair 4's upper half (tap 9) has zero weights and reads tap 0's data
+      int offT[5];
+#pragma unroll
+      for (int pr = 0; pr < 5; ++pr) {
+        int t = 2 * pr + (hi >> 1);
+        if (t > 8) t = 0;
+        const int dy = t / 3, dx = t - dy * 3;
+        offT[pr] = swz((wave * RW + dy) * kPitch + col + dx, col + dx, hi & 1);
+      }
+      stage_w<BN>(p, Lw, n0, ch, 0, 5, true);
+      __syncthreads();
+#pragma unroll
+      for (int pr = 0; pr < 5; ++pr) {
+        bf16x8 a[NT], bb[RW];
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+          a[j] = *reinterpret_cast<const bf16x8 *>(Lw + offA + (pr * BN + j * 16) * 32);
+#pragma unroll
+        for (int r = 0; r < RW; ++r) bb[r] = *reinterpret_cast<const bf16x8 *>(Li + offT[pr] + r * ROWB);
+#pragma unroll
+        for (int r = 0; r < RW; ++r)
+#pragma unroll
+          for (int j = 0; j < NT; ++j)
+            acc[r][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[j], bb[r], acc[r][j], 0, 0, 0);
+      }
+      continue;
+    }
+    if constexpr (!WSPLIT) {
+      stage_w<BN>(p, Lw, n0, ch, 0, 9, false);
+      __syncthreads();
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const int dy = t / 3, dx = t % 3;
+        bf16x8 a[NT], bb[RW];
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+          a[j] = *reinterpret_cast<const bf16x8 *>(Lw + offA + (t * BN + j * 16) * 32);
+#pragma unroll
+        for (int r = 0; r < RW; ++r)
+          bb[r] = *reinterpret_cast<const bf16x8 *>(Li + offB[dx] + (r + dy) * ROWB);
+#pragma unroll
+        for (int r = 0; r < RW; ++r)
+#pragma unroll
+          for (int j = 0; j < NT; ++j)
+            acc[r][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[j], bb[r], acc[r][j], 0, 0, 0);
+      }
+    } else {
+#pragma unroll
+      for (int dy = 0; dy < 3; ++dy) {
+        if (dy > 0) __syncthreads();
+        stage_w<BN>(p, Lw, n0, ch, dy * 3, 3, false);
+        __syncthreads();
+#pragma unroll
+        for (int dx = 0; dx < 3; ++dx) {
+          bf16x8 a[NT], bb[RW];
+#pragma unroll
+          for (int j = 0; j < NT; ++j)
+            a[j] = *reinterpret_cast<const bf16x8 *>(Lw + offA + (dx * BN + j * 16) * 32);
+#pragma unroll
+          for (int r = 0; r < RW; ++r)
+            bb[r] = *reinterpret_cast<const bf16x8 *>(Li + offB[dx] + (r + dy) * ROWB);
+#pragma unroll
+          for (int r = 0; r < RW; ++r)
+#pragma unroll
+            for (int j = 0; j < NT; ++j)
+              acc[r][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[j], bb[r], acc[r][j], 0, 0, 0);
+        }
+      }
+    }
+  }
+
+  // ---- epilogue (epilogue.h)
+  __syncthreads();
+  float *T = reinterpret_cast<float *>(smem);
+  constexpr int LD = BN + 4;
+#pragma unroll
+  for (int r = 0; r < RW; ++r)
+#pragma unroll
+    for (int j = 0; j < NT; ++j)
+      epi::put4(p, T, LD, (wave * RW + r) * 16 + col, j * 16 + hi * 4, Lc, acc[r][j]);
+  __syncthreads();
+  epi::store_tile<TOUT, epi::ipt(TH * 16, BN, 256)>(p, T, LD, TH * 16, n0, min(BN, p.cout - n0), Lc, BN,
+                                                     [&](int l, int &oy, int &ox) {
+    oy = oy0 + (l >> 4);
+    ox = ox0 + (l & 15);
+    return oy < p.Ho && ox < p.Wo;
+  });
+}
+
+// ---------------------------------------------------------------------------
+// Persistent variant with resident weights (Cin <= 128 and a weight slice of
+// <= 84 KB).  Each workgroup keeps the packed weights of one BN-wide n-block
+// in LDS for the whole launch and walks spatial tiles s, s + G, ...  Input
+// tiles are double-buffered in LDS and filled by LDS-DMA
+// (buffer_load_dwordx4 ... lds): the next tile's load is issued before the
+// current tile's MFMAs and waited for only after them, with raw s_barriers
+// so no __syncthreads() fence drains it early.  An LDS-DMA instruction fills
+// 1 KB linearly (16 pixel rows x 4 slots), so the slot swizzle is applied to
+// the per-lane SOURCE address; halo pixels outside the image, the pitch
+// padding and a tail chunk's upper slots read out of the buffer's range,
+// which the hardware returns as zeros.
+// LDS: weights [KS][BN][32] (KS = 9 per 32-channel chunk + 5 tap pairs for a
+// 16-channel tail) | buffer 0 | buffer 1 | epilogue constants; a buffer holds
+// one [IH][20][32] image per chunk (1 KB-padded) and, after its tile's
+// MFMAs, that tile's fp32 epilogue tile.
+template <int NCH, bool TAIL, int BN>
+__device__ __forceinline__ void stage_resident_w(const C3 &p, uint16_t *Lw, int n0) {
+  constexpr int KS = 9 * NCH + (TAIL ? 5 : 0);
+  constexpr int items = KS * BN * 4;
+  constexpr int kB = 4;
+  for (int base = threadIdx.x; base < items; base += 256 * kB) {
+    u16x8 v[kB];
+#pragma unroll
+    for (int u = 0; u < kB; ++u) {
+      const int it = base + u * 256;
+      zero8(v[u]);
+      if (it >= items) continue;
+      const int row = it >> 2, sl = it & 3;
+      const int ks = row / BN, n = n0 + row - ks * BN;
+      if (n >= p.cout) continue;
+      int tap, c;
+      if (ks < 9 * NCH) {
+        tap = ks % 9;
+        c = (ks / 9) * 32 + sl * 8;
+      } else {
+        tap = 2 * (ks - 9 * NCH) + (sl >> 1);
+        c = NCH * 32 + (sl & 1) * 8;
+      }
+      if (tap < 9) v[u] = *reinterpret_cast<const u16x8 *>(p.w + ((int64_t)n * 9 + tap) * p.cinp + c);
+    }
+#pragma unroll
+    for (int u = 0; u < kB; ++u) {
+      const int it = base + u * 256;
+      if (it >= items) continue;
+      const int row = it >> 2;
+      *reinterpret_cast<u16x8 *>(Lw + swz(row, row, it & 3)) = v[u];
+    }
+  }
+}
+
+template <int NCH, bool TAIL, int BN, int TH>
+struct ResGeom {
+  static constexpr int NIMG = NCH + (TAIL ? 1 : 0);
+  static constexpr int KS = 9 * NCH + (TAIL ? 5 : 0);
+  static constexpr int IH = TH + 2;
+  static constexpr int IMG_KB = (IH * kPitch * 64 + 1023) / 1024;  // LDS-DMA blocks per image
+  static constexpr size_t IMGB = (size_t)IMG_KB * 1024;
+  static constexpr size_t TB = (size_t)TH * 16 * (BN + 4) * 4;     // epilogue tile
+  static constexpr size_t BUF = NIMG * IMGB > TB ? NIMG * IMGB : ((TB + 1023) / 1024) * 1024;
+  static constexpr size_t WB = (size_t)KS * BN * 64;
+  static constexpr size_t LC = WB + 2 * BUF;                        // epilogue constants
+  static constexpr size_t LDS = LC + (size_t)epi::consts_floats(BN) * 4;
+};
+
+__device__ __forceinline__ void wait_lgkm() { __builtin_amdgcn_s_waitcnt(0xC07F); }      // lgkmcnt(0)
+__device__ __forceinline__ void wait_vm_lgkm() { __builtin_amdgcn_s_waitcnt(0x0070); }   // vmcnt(0) lgkmcnt(0)
+
+template <int NCH, bool TAIL, int BN, int TH, typename TOUT, bool RES>
+__global__ void __launch_bounds__(256) conv3x3_res_kernel(C3 p) {
+  typedef ResGeom<NCH, TAIL, BN, TH> G_;
+  constexpr int RW = TH / 4, NT = BN / 16;
+  constexpr int ROWB = kPitch * 32;             // elements per halo row
+  constexpr int IMG = (int)(G_::IMGB / 2);      // elements per chunk image
+  constexpr int NDMA = G_::NIMG * G_::IMG_KB;   // LDS-DMA instructions per tile
+  constexpr int DPW = (NDMA + 3) / 4;           // per wave
+  constexpr int LD = BN + 4;
+  extern __shared__ __align__(16) unsigned char smem[];
+  uint16_t *Lw = reinterpret_cast<uint16_t *>(smem);
+  unsigned char *Buf0 = smem + G_::WB;
+  float *Lc = reinterpret_cast<float *>(smem + G_::LC);
+
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int col = lane & 15, hi = lane >> 4;
+  const int n0 = (blockIdx.x % p.nblk_n) * BN;
+  const int G = gridDim.x / p.nblk_n;
+  const int ntiles = p.tiles_x * p.tiles_y;
+  int s = blockIdx.x / p.nblk_n;
+  if (s >= ntiles) return;
+
+  const __amdgpu_buffer_rsrc_t rsrc =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t *>(p.x), (short)0, p.xbytes, 0x00020000);
+  const int lrow = lane >> 2, lslot = lane & 3;
+  // issue the LDS-DMA loads of tile t into buffer `buf`
+  auto issue = [&](int t, unsigned char *buf) {
+    const int oy0 = (t / p.tiles_x) * TH, ox0 = (t % p.tiles_x) * 16;
+#pragma unroll
+    for (int d = 0; d < DPW; ++d) {
+      const int i = wave + 4 * d;
+      if (i < NDMA) {
+        const int c = i / G_::IMG_KB, k = i - c * G_::IMG_KB;
+        const int r = k * 16 + lrow;                // pixel row of the image
+        const int iy = r / kPitch, ix = r - iy * kPitch;
+        const int ls = lslot ^ (((ix >> 2) & 1) << 1);
+        const int gy = oy0 - 1 + iy, gx = ox0 - 1 + ix;
+        int voff = 0x7ffffff0;                      // out of range: zeros
+        if (iy < G_::IH && ix < 18 && gy >= 0 && gy < p.H && gx >= 0 && gx < p.W && (c < NCH || ls < 2))
+          voff = ((gy * p.W + gx) * p.xcs + p.xco + c * 32 + ls * 8) * 2;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            rsrc, (__attribute__((address_space(3))) void *)(buf + c * G_::IMGB + k * 1024), 16, voff, 0, 0, 0);
+      }
+    }
+  };
+
+  // per-lane MFMA operand bases (elements within a buffer)
+  int offB[3];
+#pragma unroll
+  for (int dx = 0; dx < 3; ++dx) offB[dx] = swz(wave * RW * kPitch + col + dx, col + dx, hi);
+  int offT[5];
+#pragma unroll
+  for (int pr = 0; pr < 5; ++pr) {
+    int t = 2 * pr + (hi >> 1);
+    if (t > 8) t = 0;  // tap 9: zero weights, any finite data
+    const int dy = t / 3, dx = t - dy * 3;
+    offT[pr] = NCH * IMG + swz((wave * RW + dy) * kPitch + col + dx, col + dx, hi & 1);
+  }
+  const uint16_t *LwA = Lw + swz(col, col, hi);
+  const bool lrelu_in = p.in_op == DCVC_IN_LRELU;
+
+  int cur = 0;
+  issue(s, Buf0);
+  stage_resident_w<NCH, TAIL, BN>(p, Lw, n0);
+  epi::stage_consts(p, Lc, n0, BN);
+  wait_vm_lgkm();
+  __builtin_amdgcn_s_barrier();
+  for (;;) {
+    unsigned char *bc = Buf0 + cur * G_::BUF;
+    uint16_t *Li = reinterpret_cast<uint16_t *>(bc);
+    const int sn = s + G;
+    const bool more = sn < ntiles;
+    if (more) issue(sn, Buf0 + (cur ^ 1) * G_::BUF);
+    if (lrelu_in) {
+      // ResBlock-style input transform, in place on this tile's image
+      wait_lgkm();
+      __builtin_amdgcn_s_barrier();
+      for (int e = threadIdx.x; e < G_::NIMG * IMG / 8; e += 256) {
+        u16x8 v = reinterpret_cast<u16x8 *>(Li)[e];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float f = bf2f(v[j]);
+          v[j] = f2bf(f >= 0.f ? f : f * p.in_slope);
+        }
+        reinterpret_cast<u16x8 *>(Li)[e] = v;
+      }
+      wait_lgkm();
+      __builtin_amdgcn_s_barrier();
+    }
+
+    f32x4 acc[RW][NT];
+#pragma unroll
+    for (int r = 0; r < RW; ++r)
+#pragma unroll
+      for (int j = 0; j < NT; ++j) acc[r][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const int dy = t / 3, dx = t % 3;
+        bf16x8 a[NT], bb[RW];
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+          a[j] = *reinterpret_cast<const bf16x8 *>(LwA + ((c * 9 + t) * BN + j * 16) * 32);
+#pragma unroll
+        for (int r = 0; r < RW; ++r)
+          bb[r] = *reinterpret_cast<const bf16x8 *>(Li + c * IMG + offB[dx] + (r + dy) * ROWB);
+#pragma unroll
+        for (int r = 0; r < RW; ++r)
+#pragma unroll
+          for (int j = 0; j < NT; ++j)
+            acc[r][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[j], bb[r], acc[r][j], 0, 0, 0);
+      }
+    }
+    if constexpr (TAIL) {
+#pragma unroll
+      for (int pr = 0; pr < 5; ++pr) {
+        bf16x8 a[NT], bb[RW];
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+          a[j] = *reinterpret_cast<const bf16x8 *>(LwA + ((9 * NCH + pr) * BN + j * 16) * 32);
+#pragma unroll
+        for (int r = 0; r < RW; ++r) bb[r] = *reinterpret_cast<const bf16x8 *>(Li + offT[pr] + r * ROWB);
+#pragma unroll
+        for (int r = 0; r < RW; ++r)
+#pragma unroll
+          for (int j = 0; j < NT; ++j)
+            acc[r][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[j], bb[r], acc[r][j], 0, 0, 0);
+      }
+    }
+    wait_lgkm();
+    __builtin_amdgcn_s_barrier();  // every wave is done reading this tile's images
+    float *T = reinterpret_cast<float *>(bc);
+#pragma unroll
+    for (int r = 0; r < RW; ++r)
+#pragma unroll
+      for (int j = 0; j < NT; ++j)
+        epi::put4(p, T, LD, (wave * RW + r) * 16 + col, j * 16 + hi * 4, Lc, acc[r][j]);
+    wait_vm_lgkm();                // T written; the next tile's LDS-DMA has landed
+    __builtin_amdgcn_s_barrier();
+    const int oy0 = (s / p.tiles_x) * TH, ox0 = (s % p.tiles_x) * 16;
+    epi::store_tile<TOUT, epi::ipt(TH * 16, BN, 256), RES>(p, T, LD, TH * 16, n0, min(BN, p.cout - n0), Lc, BN,
+                                                            [&](int l, int &oy, int &ox) {
+                                                         oy = oy0 + (l >> 4);
+                                                         ox = ox0 + (l & 15);
+                                                         return oy < p.Ho && ox < p.Wo;
+                                                       });
+    if (!more) break;
+    wait_lgkm();
+    __builtin_amdgcn_s_barrier();  // T read: this buffer may be refilled
+    s = sn;
+    cur ^= 1;
+  }
+}
+
+int g_cus = 0;
+int g_resident = 1;  // 0: off, 1: measured-best shapes, 2: every fitting shape
+
+template <int NCH, bool TAIL, int BN, int TH, typename TOUT>
+int launch_res(C3 p, hipStream_t st) {
+  constexpr size_t lds = ResGeom<NCH, TAIL, BN, TH>::LDS;
+  if constexpr (lds > 160 * 1024) {
+    return DCVC_HIP_EUNSUPPORTED;
+  } else {
+    p.tiles_x = (p.Wo + 15) / 16;
+    p.tiles_y = (p.Ho + TH - 1) / TH;
+    p.nblk_n = (p.cout + BN - 1) / BN;
+    const int64_t ntiles = (int64_t)p.tiles_x * p.tiles_y;
+    if (ntiles <= 0) return DCVC_HIP_OK;
+    if (g_cus <= 0) {
+      int dev = 0;
+      hipDeviceProp_t prop;
+      if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess)
+        return DCVC_HIP_ELAUNCH;
+      g_cus = prop.multiProcessorCount;
+    }
+    const int per_cu = (int)((160 * 1024) / lds) >= 2 ? 2 : 1;
+    int64_t G = ((int64_t)g_cus * per_cu + p.nblk_n - 1) / p.nblk_n;
+    if (G > ntiles) G = ntiles;
+    auto kern = (p.res || p.res2) ? conv3x3_res_kernel<NCH, TAIL, BN, TH, TOUT, true>
+                                  : conv3x3_res_kernel<NCH, TAIL, BN, TH, TOUT, false>;
+    if (lds > 64 * 1024)
+      (void)hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(kern, dim3((unsigned)(G * p.nblk_n)), dim3(256), lds, st, p);
+    DCVC_LAUNCH_CHECK();
+    return DCVC_HIP_OK;
+  }
+}
+
+constexpr size_t kResW = 84 * 1024;  // resident weight budget
+
+// BN: fewest padded output channels among slices that fit kResW (wider on
+// ties); TH: 8 when both buffers fit beside the weights, else 4.
+template <int NCH, bool TAIL, int BN, typename TOUT>
+int pick_res_th(const C3 &p, hipStream_t st) {
+  if constexpr (ResGeom<NCH, TAIL, BN, 8>::LDS <= 160 * 1024) return launch_res<NCH, TAIL, BN, 8, TOUT>(p, st);
+  return launch_res<NCH, TAIL, BN, 4, TOUT>(p, st);
+}
+
+template <int NCH, bool TAIL, typename TOUT>
+int pick_res(const C3 &p, hipStream_t st) {
+  constexpr int KS = 9 * NCH + (TAIL ? 5 : 0);
+  static const int cand[4] = {16, 32, 48, 64};
+  int best = 0;
+  long best_pad = -1;
+  for (int bn : cand) {
+    if ((size_t)KS * bn * 64 > kResW) continue;
+    const long pad = ((p.cout + bn - 1) / bn) * (long)bn - p.cout;
+    if (best_pad < 0 || pad < best_pad || (pad == best_pad && bn > best)) {
+      best = bn;
+      best_pad = pad;
+    }
+  }
+  switch (best) {
+    case 16: return pick_res_th<NCH, TAIL, 16, TOUT>(p, st);
+    case 32: return pick_res_th<NCH, TAIL, 32, TOUT>(p, st);
+    case 48: return pick_res_th<NCH, TAIL, 48, TOUT>(p, st);
+    case 64: return pick_res_th<NCH, TAIL, 64, TOUT>(p, st);
+    default: return DCVC_HIP_EUNSUPPORTED;
+  }
+}
+
+// Measured on MI355X (scripts/conv_microbench.py): the resident variant wins
+// for 96-input-channel layers (96->48 at 1080p: 334 vs 375 us; 96->96 at
+// 272x480: 50 vs 54 us) and loses where the per-workgroup kernel keeps two
+// workgroups per CU (48/64 channels) or where the weight budget forces
+// BN = 32 (128 input channels); only the winning shapes are routed here.
+template <typename TOUT>
+int dispatch_res(const C3 &p, hipStream_t st) {
+  if (g_resident >= 2) {  // every fitting shape (A/B experiments)
+    switch (p.cin) {
+      case 16: return pick_res<0, true, TOUT>(p, st);
+      case 32: return pick_res<1, false, TOUT>(p, st);
+      case 48: return pick_res<1, true, TOUT>(p, st);
+      case 64: return pick_res<2, false, TOUT>(p, st);
+      case 80: return pick_res<2, true, TOUT>(p, st);
+      case 128: return pick_res<4, false, TOUT>(p, st);
+      default: break;
+    }
+  }
+  if (p.cin == 96 && p.cout >= 48) return pick_res<3, false, TOUT>(p, st);
+  return DCVC_HIP_EUNSUPPORTED;
+}
+
+
+template <int BN, int TH>
+constexpr bool wsplit() { return BN >= 96; }
+
+template <int BN, int TH>
+size_t lds_bytes(bool tail) {
+  const size_t in = (size_t)(TH + 2) * kPitch * 64;
+  size_t wrows = wsplit<BN, TH>() ? 3 : 9;
+  if (tail && wrows < 5) wrows = 5;
+  const size_t stage = in + wrows * BN * 64;
+  const size_t epi = (size_t)TH * 16 * (BN + 4) * 4;
+  return stage > epi ? stage : epi;
+}
+
+template <int BN, int TH, typename TOUT>
+int launch(C3 p, hipStream_t st) {
+  p.tiles_x = (p.Wo + 15) / 16;
+  p.tiles_y = (p.Ho + TH - 1) / TH;
+  const int64_t blocks = (int64_t)p.tiles_x * p.tiles_y * ((p.cout + BN - 1) / BN);
+  if (blocks <= 0) return DCVC_HIP_OK;
+  p.lc_off = (int)((lds_bytes<BN, TH>((p.cin & 31) == 16) + 15) & ~(size_t)15);
+  const size_t lds = p.lc_off + epi::consts_floats(BN) * 4;
+  if (lds > 160 * 1024) return DCVC_HIP_EUNSUPPORTED;
+  auto kern = conv3x3_kernel<BN, TH, wsplit<BN, TH>(), TOUT>;
+  if (lds > 64 * 1024)
+    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(256), lds, st, p);
+  DCVC_LAUNCH_CHECK();
+  return DCVC_HIP_OK;
+}
+
+// TH: 16 rows when the grid still has >= 1024 workgroups (BN <= 64), else 8, else 4
+template <int BN, typename TOUT>
+int pick_th(const C3 &p, hipStream_t st) {
+  const int64_t tx = (p.Wo + 15) / 16, tn = (p.cout + BN - 1) / BN;
+  auto blocks = [&](int th) { return tx * ((p.Ho + th - 1) / th) * tn; };
+  if (BN <= 64 && blocks(16) >= 1024) return launch<BN, 16, TOUT>(p, st);
+  if (blocks(8) >= 512) return launch<BN, 8, TOUT>(p, st);
+  return launch<BN, 4, TOUT>(p, st);
+}
+
+template <typename TOUT>
+int pick_bn(const C3 &p, hipStream_t st) {
+  static const int cand[6] = {16, 32, 48, 64, 96, 128};
+  int best = 16;
+  long best_pad = -1;
+  for (int bn : cand) {
+    const long pad = ((p.cout + bn - 1) / bn) * (long)bn - p.cout;
+    if (best_pad < 0 || pad < best_pad || (pad == best_pad && bn > best)) {
+      best = bn;
+      best_pad = pad;
+    }
+  }
+  switch (best) {
+    case 16: return pick_th<16, TOUT>(p, st);
+    case 32: return pick_th<32, TOUT>(p, st);
+    case 48: return pick_th<48, TOUT>(p, st);
+    case 64: return pick_th<64, TOUT>(p, st);
+    case 96: return pick_th<96, TOUT>(p, st);
+    default: return pick_th<128, TOUT>(p, st);
+  }
+}
+
+}  // namespace
+
+// Called by dcvc_conv2d (after its argument validation) for 3x3 / stride 1 /
+// pad 1 convs with bf16 input and compute; DCVC_HIP_EUNSUPPORTED sends the
+// call to the generic kernel.
+extern "C" int dcvc_internal_conv3x3(const dcvc_conv_args *a, void *stream) {
+  if (a->kh != 3 || a->kw != 3 || a->stride != 1 || a->pad != 1 || a->compute != DCVC_BF16)
+    return DCVC_HIP_EUNSUPPORTED;
+  if (a->x.dtype != DCVC_BF16 || (a->in_op != DCVC_IN_NONE && a->in_op != DCVC_IN_LRELU))
+    return DCVC_HIP_EUNSUPPORTED;
+  if (a->cin % 16 || a->x.cstride % 8 || a->x.coff % 8 || ((uintptr_t)a->x.ptr & 15))
+    return DCVC_HIP_EUNSUPPORTED;
+  if ((int64_t)a->x.H * a->x.W * a->x.cstride * 2 >= ((int64_t)1 << 31) - 16) return DCVC_HIP_EUNSUPPORTED;
+  C3 p{};
+  p.x = reinterpret_cast<const uint16_t *>(a->x.ptr);
+  p.H = a->x.H;
+  p.W = a->x.W;
+  p.xcs = a->x.cstride;
+  p.xco = a->x.coff;
+  p.xbytes = a->x.H * a->x.W * a->x.cstride * 2;
+  p.w = reinterpret_cast<const uint16_t *>(a->w);
+  p.cinp = (a->cin + 31) / 32 * 32;
+  p.bias = a->bias;
+  p.y = a->y.ptr;
+  p.ycs = a->y.cstride;
+  p.yco = a->y.coff;
+  p.cin = a->cin;
+  p.cout = a->cout;
+  p.in_op = a->in_op;
+  p.in_slope = a->in_slope;
+  p.act = a->act;
+  p.slope = a->slope;
+  p.shuffle = a->shuffle;
+  p.scale = a->scale;
+  p.Ho = a->x.H;
+  p.Wo = a->x.W;
+  p.Wout = a->y.W;
+  if (a->res.ptr) {
+    p.res = a->res.ptr;
+    p.rcs = a->res.cstride;
+    p.rco = a->res.coff;
+  }
+  if (a->res2.ptr) {
+    p.res2 = a->res2.ptr;
+    p.r2cs = a->res2.cstride;
+    p.r2co = a->res2.coff;
+  }
+  bool vo = (p.ycs % 8 == 0) && (p.yco % 8 == 0) && (((uintptr_t)p.y & 15) == 0);
+  if (a->res.ptr) vo = vo && (p.rcs % 8 == 0) && (p.rco % 8 == 0) && (((uintptr_t)p.res & 15) == 0);
+  if (a->res2.ptr) vo = vo && (p.r2cs % 8 == 0) && (p.r2co % 8 == 0) && (((uintptr_t)p.res2 & 15) == 0);
+  p.vec_out = vo ? 1 : 0;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (g_resident) {
+    const int r = a->y.dtype == DCVC_F32 ? dispatch_res<float>(p, st) : dispatch_res<uint16_t>(p, st);
+    if (r != DCVC_HIP_EUNSUPPORTED) return r;
+  }
+  if (a->y.dtype == DCVC_F32) return pick_bn<float>(p, st);
+  return pick_bn<uint16_t>(p, st);
+}
+
+// dcvc_set_option("conv3x3_resident", 0/1) (A/B switch, via conv.hip)
+extern "C" void dcvc_internal_conv3x3_resident(int v) { g_resident = v; }

@@ -10,8 +10,10 @@
 //
 // One workgroup = 4 waves owns an 8x16-pixel output tile.  The input tile,
 // t1, d, dc and one 64-wide slice of the FFN hidden layer live in LDS as
-// bf16 [pixel][channel] images (16-byte slots XOR-swizzled per row); weights
-// are read as MFMA A fragments straight from global memory (tiny, L2/L1-hot).
+// bf16 [pixel][channel] images (16-byte slots XOR-swizzled per row); each
+// phase's weights are staged through an LDS image 64 input channels at a
+// time (L2-hot: every workgroup reads the same few KB), the output tile is
+// assembled in LDS and written with whole-line 16-byte stores.
 // HBM traffic is one read of x (with halo) and one write of out: the 4x-wide
 // FFN intermediate and the three other intermediates never leave the CU.
 // Every GEMM is D[n][pixel] = W[n][k] X[pixel][k] on v_mfma_f32_16x16x32_bf16;
@@ -363,14 +365,11 @@ __global__ void __launch_bounds__(256) dcb_kernel(DcbP p) {
     }
   }
 
-  // ---- P5: out = dc + act(acc + bf2) [* scale] -> y
+  // ---- P5: out = dc + act(acc + bf2) [* scale] as bf16 -> Cs (free since
+  // the last FFN slice's trailing barrier), then whole-line stores to y
 #pragma unroll
   for (int i = 0; i < NPT; ++i) {
     const int pix = pt[i] * 16 + col;
-    const int r = pix / TW, cc = pix % TW;
-    const int gy = oy0 + r, gx = ox0 + cc;
-    if (gy >= p.H || gx >= p.W) continue;
-    uint16_t *out = p.y + ((int64_t)gy * p.W + gx) * p.ycs + p.yco;
 #pragma unroll
     for (int j = 0; j < NTO; ++j) {
       const int c = j * 16 + hi * 4;
@@ -384,8 +383,17 @@ __global__ void __launch_bounds__(256) dcb_kernel(DcbP p) {
         if (p.scale) t = t * p.scale[c + q];
         o[q] = f2bf(t);
       }
-      *reinterpret_cast<u16x4 *>(out + c) = o;
+      *reinterpret_cast<u16x4 *>(Cs + img<RLO>(pix, c)) = o;
     }
+  }
+  __syncthreads();
+  constexpr int NSO = COUT / 8;
+  for (int it = threadIdx.x; it < NPI * NSO; it += 256) {
+    const int pix = it / NSO, s8 = (it % NSO) * 8;
+    const int gy = oy0 + pix / TW, gx = ox0 + pix % TW;
+    if (gy >= p.H || gx >= p.W) continue;
+    *reinterpret_cast<u16x8 *>(p.y + ((int64_t)gy * p.W + gx) * p.ycs + p.yco + s8) =
+        *reinterpret_cast<const u16x8 *>(Cs + img<RLO>(pix, s8));
   }
 }
 
@@ -440,8 +448,8 @@ extern "C" int dcvc_depthconv_block(const dcvc_dcb_args *a, void *stream) {
   if (!a || !a->x.ptr || !a->y.ptr) return DCVC_HIP_EINVAL;
   if (a->x.dtype != DCVC_BF16 || a->y.dtype != DCVC_BF16) return DCVC_HIP_EUNSUPPORTED;
   if (a->x.H != a->y.H || a->x.W != a->y.W || a->x.C != a->cin || a->y.C != a->cout) return DCVC_HIP_EINVAL;
-  if (a->x.cstride % 8 || a->x.coff % 8 || a->y.cstride % 4 || a->y.coff % 4 ||
-      ((uintptr_t)a->x.ptr & 15) || ((uintptr_t)a->y.ptr & 7))
+  if (a->x.cstride % 8 || a->x.coff % 8 || a->y.cstride % 8 || a->y.coff % 8 ||
+      ((uintptr_t)a->x.ptr & 15) || ((uintptr_t)a->y.ptr & 15))
     return DCVC_HIP_EUNSUPPORTED;
   const bool adapt = a->w_adaptor != nullptr;
   if (!adapt && a->cin != a->cout) return DCVC_HIP_EINVAL;

@@ -9,8 +9,9 @@
 // latency hides behind the matrix work.  LDS rows are 128 B (64 bf16) with
 // the 16-byte slot XOR-swizzled by (row >> 1) & 7 so the 16 lanes of an MFMA
 // operand read (16 consecutive rows, same slot) hit 16 distinct bank groups.
-// The epilogue is conv.hip's: bias, act, residual(s), scale, pixel shuffle.
+// The epilogue is epilogue.h's: bias, act, residual(s), scale, pixel shuffle.
 #include "common.h"
+#include "epilogue.h"
 
 namespace {
 
@@ -70,29 +71,11 @@ template <> struct Piece<float> {
   }
 };
 
-template <typename TOUT>
-__device__ __forceinline__ void store4(void *y, int64_t e, const float v[4]);
-template <>
-__device__ __forceinline__ void store4<float>(void *y, int64_t e, const float v[4]) {
-  *reinterpret_cast<float4 *>(reinterpret_cast<float *>(y) + e) = make_float4(v[0], v[1], v[2], v[3]);
-}
-template <>
-__device__ __forceinline__ void store4<uint16_t>(void *y, int64_t e, const float v[4]) {
-  u16x4 o;
-  o[0] = f2bf(v[0]); o[1] = f2bf(v[1]); o[2] = f2bf(v[2]); o[3] = f2bf(v[3]);
-  *reinterpret_cast<u16x4 *>(reinterpret_cast<uint16_t *>(y) + e) = o;
-}
-template <typename T>
-__device__ __forceinline__ void load4(const void *base, int64_t e, float v[4]);
-template <>
-__device__ __forceinline__ void load4<float>(const void *base, int64_t e, float v[4]) {
-  const float4 a = *reinterpret_cast<const float4 *>(reinterpret_cast<const float *>(base) + e);
-  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
-}
-template <>
-__device__ __forceinline__ void load4<uint16_t>(const void *base, int64_t e, float v[4]) {
-  const u16x4 a = *reinterpret_cast<const u16x4 *>(reinterpret_cast<const uint16_t *>(base) + e);
-  v[0] = bf2f(a[0]); v[1] = bf2f(a[1]); v[2] = bf2f(a[2]); v[3] = bf2f(a[3]);
+// staging double buffer, or the fp32 epilogue tile, whichever is larger
+template <int BM, int BN>
+__host__ __device__ constexpr size_t lds_main() {
+  return ((size_t)2 * (BM + BN) * kK * 2 > (size_t)BM * (BN + 4) * 4 ? (size_t)2 * (BM + BN) * kK * 2
+                                                                      : (size_t)BM * (BN + 4) * 4);
 }
 
 template <typename TIN, typename TOUT, int BM, int BN, int WMW>
@@ -106,6 +89,7 @@ __global__ void __launch_bounds__(256) gemm1x1_kernel(G1 p) {
   extern __shared__ __align__(16) unsigned char smem[];
   uint16_t *Xs = reinterpret_cast<uint16_t *>(smem);             // [2][BM][64]
   uint16_t *Ws = Xs + 2 * BM * kK;                                // [2][BN][64]
+  float *Lc = reinterpret_cast<float *>(smem + lds_main<BM, BN>());  // bias | scale
 
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int wm = wave % WMW, wn = wave / WMW;
@@ -113,6 +97,7 @@ __global__ void __launch_bounds__(256) gemm1x1_kernel(G1 p) {
   const int m0 = tm * BM, n0 = tn * BN;
   const TIN *X = reinterpret_cast<const TIN *>(p.x);
   const int nsteps = p.cinp / kK;
+  epi::stage_consts(p, Lc, n0, BN);  // published by the first barrier below
 
   Piece<TIN> px[PX];
   u16x8 pw[PW];
@@ -208,70 +193,30 @@ __global__ void __launch_bounds__(256) gemm1x1_kernel(G1 p) {
     __syncthreads();
   }
 
-  // epilogue: lane owns pixel m and channels nb..nb+3 of each (i, j) tile
+  // epilogue (epilogue.h): fp32 tile in LDS (the loop ended on a barrier),
+  // then coalesced stores
+  float *T = reinterpret_cast<float *>(smem);
+  constexpr int LD = BN + 4;
 #pragma unroll
-  for (int i = 0; i < TM; ++i) {
-    const int m = m0 + (wm * TM + i) * 16 + col;
-    if (m >= p.M) continue;
-    const int oy = m / p.W, ox = m - oy * p.W;
+  for (int i = 0; i < TM; ++i)
 #pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int nb = n0 + (wn * TN + j) * 16 + hi * 4;
-      if (nb >= p.cout) continue;
-      float v[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        float t = acc[i][j][q];
-        if (p.bias && nb + q < p.cout) t += p.bias[nb + q];
-        v[q] = apply_act(p.act, t, p.slope);
-      }
-      if (p.vec_out && nb + 3 < p.cout) {
-        const int64_t pix = m;
-        if (p.res) {
-          float rv[4];
-          load4<TOUT>(p.res, pix * p.rcs + p.rco + nb, rv);
-#pragma unroll
-          for (int q = 0; q < 4; ++q) v[q] = rv[q] + v[q];
-        }
-        if (p.res2) {
-          float rv[4];
-          load4<TOUT>(p.res2, pix * p.r2cs + p.r2co + nb, rv);
-#pragma unroll
-          for (int q = 0; q < 4; ++q) v[q] = rv[q] + v[q];
-        }
-        if (p.scale) {
-#pragma unroll
-          for (int q = 0; q < 4; ++q) v[q] = v[q] * p.scale[nb + q];
-        }
-        store4<TOUT>(p.y, pix * p.ycs + p.yco + nb, v);
-        continue;
-      }
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int n = nb + q;
-        if (n >= p.cout) continue;
-        float t = v[q];
-        int c = n, yy = oy, xx = ox;
-        if (p.shuffle) {
-          c = n >> 2;
-          yy = oy * 2 + ((n >> 1) & 1);
-          xx = ox * 2 + (n & 1);
-        }
-        const int64_t pix = (int64_t)yy * p.Wout + xx;
-        if (p.res) t = ld<TOUT>(p.res, pix * p.rcs + p.rco + c) + t;
-        if (p.res2) t = ld<TOUT>(p.res2, pix * p.r2cs + p.r2co + c) + t;
-        if (p.scale) t = t * p.scale[c];
-        st<TOUT>(p.y, pix * p.ycs + p.yco + c, t);
-      }
-    }
-  }
+    for (int j = 0; j < TN; ++j)
+      epi::put4(p, T, LD, (wm * TM + i) * 16 + col, (wn * TN + j) * 16 + hi * 4, Lc, acc[i][j]);
+  __syncthreads();
+  epi::store_tile<TOUT, epi::ipt(BM, BN, 256)>(p, T, LD, BM, n0, min(BN, p.cout - n0), Lc, BN,
+                                               [&](int l, int &oy, int &ox) {
+    const int m = m0 + l;
+    oy = m / p.W;
+    ox = m - oy * p.W;
+    return m < p.M;
+  });
 }
 
 template <typename TIN, typename TOUT, int BM, int BN, int WMW>
 int launch(G1 p, hipStream_t st) {
   p.tiles_m = (p.M + BM - 1) / BM;
   const int tiles_n = (p.cout + BN - 1) / BN;
-  const size_t lds = (size_t)2 * (BM + BN) * kK * 2;
+  const size_t lds = lds_main<BM, BN>() + epi::consts_floats(BN) * 4;
   auto kern = gemm1x1_kernel<TIN, TOUT, BM, BN, WMW>;
   if (lds > 64 * 1024)
     (void)hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
@@ -355,9 +300,9 @@ extern "C" int dcvc_internal_gemm1x1(const dcvc_conv_args *a, void *stream) {
     p.r2cs = a->res2.cstride;
     p.r2co = a->res2.coff;
   }
-  bool vo = !a->shuffle && (p.ycs % 4 == 0) && (p.yco % 4 == 0) && (((uintptr_t)p.y & 15) == 0);
-  if (a->res.ptr) vo = vo && (p.rcs % 4 == 0) && (p.rco % 4 == 0);
-  if (a->res2.ptr) vo = vo && (p.r2cs % 4 == 0) && (p.r2co % 4 == 0);
+  bool vo = (p.ycs % 8 == 0) && (p.yco % 8 == 0) && (((uintptr_t)p.y & 15) == 0);
+  if (a->res.ptr) vo = vo && (p.rcs % 8 == 0) && (p.rco % 8 == 0) && (((uintptr_t)p.res & 15) == 0);
+  if (a->res2.ptr) vo = vo && (p.r2cs % 8 == 0) && (p.r2co % 8 == 0) && (((uintptr_t)p.res2 & 15) == 0);
   p.vec_out = vo ? 1 : 0;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (xin32 && yout32) return dispatch<float, float>(p, st);

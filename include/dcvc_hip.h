@@ -91,7 +91,10 @@ int64_t dcvc_conv_pack_weights(const float *w, int cout, int cin, int kh,
                                int kw, int compute, void *out);
 int dcvc_conv2d(const dcvc_conv_args *a, void *stream);
 /* Runtime switches (testing / A-B): "gemm1x1" = 1 (default) routes 1x1
- * stride-1 bf16 convs to the double-buffered GEMM kernel. */
+ * stride-1 bf16 convs to the double-buffered GEMM kernel; "conv3x3" = 1
+ * (default) routes 3x3 stride-1 bf16 convs to the fixed-geometry kernels;
+ * "conv3x3_resident" = 1 (default) prefers its persistent resident-weight
+ * variant where the weights fit in LDS. */
 int dcvc_set_option(const char *name, int value);
 
 /*

@@ -279,6 +279,63 @@ def test_gemm1x1_equals_generic_conv(case, xdt):
     assert rel_err(back(y), ref) < 2e-2
 
 
+C3_CASES = [
+    # cin, cout, H, W, coff (input channel view offset in a wider buffer)
+    (64, 64, 37, 61, 0), (96, 192, 20, 33, 0), (128, 128, 9, 13, 0), (192, 96, 11, 70, 0),
+    (128, 192, 40, 36, 0), (96, 96, 25, 70, 0), (64, 128, 300, 20, 0),
+    (64, 3, 33, 47, 0), (32, 256, 18, 17, 32),
+    (48, 48, 40, 50, 0), (80, 48, 17, 19, 0), (16, 32, 30, 30, 0), (48, 64, 21, 35, 16),
+]
+
+
+@pytest.mark.parametrize("case", C3_CASES)
+def test_conv3x3_fixed_geometry_kernel(case):
+    """The fixed-geometry 3x3 kernel vs the generic conv kernel: bit-identical
+    when Cin % 32 == 0 (same K order), fp32-rounding-close with a 16-channel
+    tail chunk (two taps per MFMA); both vs torch fp32 with bf16 tolerance.
+    Exercises lrelu input op, bias + act, residual, scale, shuffle, f32 out,
+    a channel-offset input view and ragged tile edges."""
+    h = K()
+    cin, cout, H, W, coff = case
+    x = torch.randn(1, cin + coff + 8, H, W)
+    w = torch.randn(cout, cin, 3, 3) / (9 * cin) ** 0.5
+    b = torch.randn(cout) * 0.1
+    cw = h.ConvW(w, b, 1, h.BF16)
+    xbuf = to_act(x, h.BF16)
+    xa = xbuf.ch(coff, cin)
+    rt = torch.randn(1, cout, H, W)
+    sc = torch.rand(cout if cout % 4 else cout // 4) + 0.5
+    outs = []
+    for use, res in ((1, 2), (0, 1), (1, 0)):
+        h.set_option("conv3x3", use)
+        h.set_option("conv3x3_resident", res)
+        r = h.empty(H, W, cout, h.BF16)
+        h.copy(to_act(rt, h.F32), r)
+        y = h.conv(cw, xa, out_dtype=h.BF16, in_op=h.IN_LRELU, in_slope=0.1, act=h.ACT_LRELU, slope=0.01,
+                   res=r)
+        y2 = h.conv(cw, xa, out_dtype=h.F32, shuffle=cout % 4 == 0,
+                    scale=sc.cuda() if cout % 4 == 0 else None)
+        torch.cuda.synchronize()
+        outs.append((back(y), back(y2)))
+    h.set_option("conv3x3", 1)
+    h.set_option("conv3x3_resident", 1)
+    xs = x[:, coff:coff + cin]
+    ref = F.leaky_relu(F.conv2d(F.leaky_relu(xs.bfloat16().float(), 0.1), w, b, padding=1), 0.01) + rt
+    assert rel_err(outs[0][0], ref) < 2e-2
+    ref2 = F.conv2d(xs.bfloat16().float(), w, b, padding=1)
+    if cout % 4 == 0:
+        ref2 = F.pixel_shuffle(ref2, 2) * sc.view(1, -1, 1, 1)
+    assert rel_err(outs[0][1], ref2) < 2e-2
+    # resident-weight and per-workgroup variants run the same K order
+    assert torch.equal(outs[0][0], outs[2][0])
+    assert torch.equal(outs[0][1], outs[2][1])
+    if cin % 32 == 0:
+        assert torch.equal(outs[0][0], outs[1][0])
+        assert torch.equal(outs[0][1], outs[1][1])
+    else:
+        assert rel_err(outs[0][1], outs[1][1]) < 1e-5
+
+
 DCB_SHAPES = [(48, 32, False), (32, 64, False), (64, 128, False), (128, 128, False), (128, 64, False),
               (64, 48, False), (64, 64, False), (16, 32, True), (32, 64, True), (64, 128, True),
               (128, 128, True), (128, 64, True), (64, 16, True)]
