@@ -75,6 +75,20 @@ def make_weights(dist, rank, device):
     return isd, psd
 
 
+def max_over_ranks(dist, elapsed, device):
+    """The job's wall time: the slowest rank's (contract: MAX over ranks)."""
+    if dist is None:
+        return elapsed
+    t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return t.item()
+
+
+def shard_seed(rank):
+    """Sequence of rank r: its own synthetic sequence (weak scaling)."""
+    return 1 + rank
+
+
 def cpu_baseline(isd, psd, args):
     """Oracle (PyTorch fp32 CPU restatement, pinned to the reference) on a
     bounded sample: one I-frame (untimed) then one P-frame encode+decode in
@@ -124,6 +138,27 @@ def cpu_baseline(isd, psd, args):
                       f"scaled x{area:.1f} by area to 1088x1920, GOP {gop} average"}
 
 
+def pmc_traffic(kname):
+    """HBM bytes per launch of `kname` (instantiation@grid, which fixes the
+    launch geometry) from the committed rocprofv3 PMC summary
+    (profiles/*_pmc.json, written by scripts/pmc_summary.py from separate
+    FETCH_SIZE / WRITE_SIZE passes, FETCH_SIZE doubled per the gfx950
+    calibration); None when no summary has this kernel."""
+    import glob
+    for path in sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)),
+                                              "profiles", "*_pmc.json")), reverse=True):
+        try:
+            with open(path) as f:
+                d = json.load(f)
+        except (OSError, ValueError):
+            continue
+        for e in d.get("kernels", []):
+            if e.get("kernel") == kname and e.get("hbm_bytes_per_launch"):
+                return {"hbm_bytes_per_launch": e["hbm_bytes_per_launch"], "source": os.path.basename(path),
+                        "rocprof_avg_launch_us": e.get("avg_us")}
+    return None
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -152,7 +187,7 @@ def main():
     h, w = args.height, args.width
     H, W = (h + 15) // 16 * 16, (w + 15) // 16 * 16
     nframes = args.warmup + args.steps
-    frames = [torch.from_numpy(moving_pattern(h, w, t, seed=1 + rank)).to(device) for t in range(nframes)]
+    frames = [torch.from_numpy(moving_pattern(h, w, t, seed=shard_seed(rank))).to(device) for t in range(nframes)]
     out_dir = f"/dev/shm/dcvc_bench_{os.getpid()}"
     os.makedirs(out_dir, exist_ok=True)
     x = K.empty(H, W, 3, K.F32, device)
@@ -189,14 +224,12 @@ def main():
     torch.cuda.synchronize(device)
     if dist is not None:
         dist.barrier()
-    elapsed = time.time() - t0
-    if dist is not None:
-        t = torch.tensor([elapsed], device=device)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = t.item()
+    elapsed = max_over_ranks(dist, time.time() - t0, device)
 
-    # ---- roofline of the dominant kernel family, from per-launch HIP events
-    # recorded on the stream the kernels run on, over one extra P-frame
+    # ---- roofline of the dominant kernel, from per-launch HIP events recorded
+    # on the stream the kernels run on, over one extra P-frame.  "Dominant" =
+    # the (kernel instantiation, layer shape) with the most time per P-frame;
+    # its bound is the larger of its MFMA time and its HBM time at peak.
     roof = None
     if not args.no_roofline and rank == 0:
         K.PROFILE = []
@@ -205,34 +238,49 @@ def main():
         fam, shapes = {}, {}
         for f, e0, e1, fl, nb, key in K.PROFILE:
             dt = e0.elapsed_time(e1) * 1e-3
-            for tab, k in ((fam, f), (shapes, f + " " + key)):
+            for tab, k in ((fam, f), (shapes, f + " " + key if "|" not in key else key)):
                 d = tab.setdefault(k, [0.0, 0, 0, 0])
                 d[0] += dt
                 d[1] += fl
                 d[2] += nb
                 d[3] += 1
         K.PROFILE = None
+        rows = sorted(shapes.items(), key=lambda kv: -kv[1][0])
         if args.profile_out:
-            rows = sorted(shapes.items(), key=lambda kv: -kv[1][0])
             with open(args.profile_out, "w") as f:
                 json.dump([{"op": k, "ms": round(v[0] * 1e3, 4), "n": v[3],
                             "tflops": round(v[1] / max(v[0], 1e-12) / 1e12, 2),
                             "gbs": round(v[2] / max(v[0], 1e-12) / 1e9, 1)} for k, v in rows], f, indent=0)
-        dom = max(fam, key=lambda k: fam[k][0])
-        tsec, fl, nb, n = fam[dom]
-        if dom == "conv":
+        key, (tsec, fl, nb, n) = rows[0]
+        peak_f = PEAK_BF16_TFLOPS if args.precision == "fast" else PEAK_F32_TFLOPS
+        t_mfma, t_hbm = fl / (peak_f * 1e12), nb / (PEAK_HBM_GBS * 1e9)
+        if t_mfma >= t_hbm:
             ach = fl / tsec / 1e12
-            peak = PEAK_BF16_TFLOPS if args.precision == "fast" else PEAK_F32_TFLOPS
-            roof = {"bound": "mfma", "achieved": round(ach, 3), "peak": peak, "unit": "TFLOP/s",
-                    "frac": round(ach / peak, 5), "traffic": None}
+            roof = {"bound": "mfma", "achieved": round(ach, 3), "peak": peak_f, "unit": "TFLOP/s",
+                    "frac": round(ach / peak_f, 5)}
         else:
             ach = nb / tsec / 1e9
             roof = {"bound": "hbm", "achieved": round(ach, 2), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                    "frac": round(ach / PEAK_HBM_GBS, 5), "traffic": None}
-        roof["kernel"] = dom
-        roof["launches"] = n
+                    "frac": round(ach / PEAK_HBM_GBS, 5)}
+        kname, _, shape = key.partition(" | ")
+        tr = pmc_traffic(kname)
+        roof["traffic"] = tr["hbm_bytes_per_launch"] if tr else None
+        if tr:
+            roof["traffic_source"] = tr["source"]
+            roof["rocprof_avg_launch_us"] = tr["rocprof_avg_launch_us"]
+        roof["kernel"] = kname
+        roof["layer"] = shape
+        roof["launches_per_P_frame"] = n
         roof["avg_launch_us"] = round(tsec / n * 1e6, 2)
+        roof["algorithmic_per_launch"] = {"flop": fl // n, "bytes": nb // n}
         roof["families_ms_per_P_frame"] = {k: round(v[0] * 1e3, 3) for k, v in fam.items()}
+        # whole-frame layer roofline: sum over launches of max(F/P, B/BW)
+        t_all = sum(v[0] for v in shapes.values())
+        t_roof = sum(max(v[1] / (peak_f * 1e12), v[2] / (PEAK_HBM_GBS * 1e9)) for v in shapes.values())
+        roof["P_frame_kernels"] = {"gpu_ms": round(t_all * 1e3, 3), "roofline_ms": round(t_roof * 1e3, 3),
+                                   "frac": round(t_roof / max(t_all, 1e-12), 4),
+                                   "tflop": round(sum(v[1] for v in shapes.values()) / 1e12, 3),
+                                   "gbytes": round(sum(v[2] for v in shapes.values()) / 1e9, 2)}
 
     if rank == 0:
         n_i = kinds[args.warmup:].count("I")

@@ -50,6 +50,16 @@ __device__ __forceinline__ float apply_act(int act, float v, float slope) {
   }
 }
 
+// Name of the last kernel instantiation launched by a dcvc_conv2d /
+// dcvc_depthconv_block call on this host thread, spelled as rocprofv3 prints
+// it ("conv3x3_kernel<48, 16, false, unsigned short>"), so per-launch HIP-event
+// timings can be matched to a rocprof kernel summary (dcvc_last_kernel).
+void dcvc_note_kernel(const char *fmt, ...);
+template <typename T> constexpr const char *tname();
+template <> constexpr const char *tname<float>() { return "float"; }
+template <> constexpr const char *tname<uint16_t>() { return "unsigned short"; }
+inline const char *bname(bool b) { return b ? "true" : "false"; }
+
 #define DCVC_LAUNCH_CHECK()                          \
   do {                                               \
     hipError_t e__ = hipGetLastError();              \

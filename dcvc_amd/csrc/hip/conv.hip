@@ -19,7 +19,20 @@
 #include "common.h"
 #include "epilogue.h"
 
+#include <cstdarg>
+#include <cstdio>
 #include <cstring>
+
+static thread_local char g_last_kernel[192];
+
+void dcvc_note_kernel(const char *fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  std::vsnprintf(g_last_kernel, sizeof(g_last_kernel), fmt, ap);
+  va_end(ap);
+}
+
+extern "C" const char *dcvc_last_kernel(void) { return g_last_kernel; }
 
 namespace {
 
@@ -383,6 +396,8 @@ int launch(const ConvP &p0, hipStream_t st) {
   if (blocks <= 0) return DCVC_HIP_OK;
   if (blocks > 0x7fffffff) return DCVC_HIP_EINVAL;
   auto kern = conv_kernel<TIN, TOUT, F32, BN, TH>;
+  dcvc_note_kernel("conv_kernel<%s, %s, %s, %d, %d>@%lld", tname<TIN>(), tname<TOUT>(), bname(F32), BN, TH,
+                   (long long)blocks * 256);
   if (lds > 64 * 1024)
     (void)hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);

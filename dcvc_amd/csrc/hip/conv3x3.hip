@@ -526,8 +526,11 @@ int launch_res(C3 p, hipStream_t st) {
     const int per_cu = (int)((160 * 1024) / lds) >= 2 ? 2 : 1;
     int64_t G = ((int64_t)g_cus * per_cu + p.nblk_n - 1) / p.nblk_n;
     if (G > ntiles) G = ntiles;
-    auto kern = (p.res || p.res2) ? conv3x3_res_kernel<NCH, TAIL, BN, TH, TOUT, true>
-                                  : conv3x3_res_kernel<NCH, TAIL, BN, TH, TOUT, false>;
+    const bool res = p.res || p.res2;
+    auto kern = res ? conv3x3_res_kernel<NCH, TAIL, BN, TH, TOUT, true>
+                    : conv3x3_res_kernel<NCH, TAIL, BN, TH, TOUT, false>;
+    dcvc_note_kernel("conv3x3_res_kernel<%d, %s, %d, %d, %s, %s>@%lld", NCH, bname(TAIL), BN, TH, tname<TOUT>(),
+                     bname(res), (long long)G * p.nblk_n * 256);
     if (lds > 64 * 1024)
       (void)hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -616,6 +619,8 @@ int launch(C3 p, hipStream_t st) {
   const size_t lds = p.lc_off + epi::consts_floats(BN) * 4;
   if (lds > 160 * 1024) return DCVC_HIP_EUNSUPPORTED;
   auto kern = conv3x3_kernel<BN, TH, wsplit<BN, TH>(), TOUT>;
+  dcvc_note_kernel("conv3x3_kernel<%d, %d, %s, %s>@%lld", BN, TH, bname(wsplit<BN, TH>()), tname<TOUT>(),
+                   (long long)blocks * 256);
   if (lds > 64 * 1024)
     (void)hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);

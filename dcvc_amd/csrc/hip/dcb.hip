@@ -412,6 +412,8 @@ int run(DcbP p, hipStream_t st) {
   const size_t lds = lds_bytes<CIN, COUT, GATED, ADAPT>();
   if (lds > 160 * 1024) return DCVC_HIP_EUNSUPPORTED;
   auto kern = dcb_kernel<CIN, COUT, GATED, ADAPT>;
+  dcvc_note_kernel("dcb_kernel<%d, %d, %s, %s>@%lld", CIN, COUT, bname(GATED), bname(ADAPT),
+                   (long long)p.tiles_x * tiles_y * 256);
   if (lds > 64 * 1024)
     (void)hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);

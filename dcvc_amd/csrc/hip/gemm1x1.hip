@@ -218,6 +218,8 @@ int launch(G1 p, hipStream_t st) {
   const int tiles_n = (p.cout + BN - 1) / BN;
   const size_t lds = lds_main<BM, BN>() + epi::consts_floats(BN) * 4;
   auto kern = gemm1x1_kernel<TIN, TOUT, BM, BN, WMW>;
+  dcvc_note_kernel("gemm1x1_kernel<%s, %s, %d, %d, %d>@%lld", tname<TIN>(), tname<TOUT>(), BM, BN, WMW,
+                   (long long)p.tiles_m * tiles_n * 256);
   if (lds > 64 * 1024)
     (void)hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);

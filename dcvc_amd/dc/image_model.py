@@ -60,6 +60,16 @@ class IntraNoAR:
             ctx.check_strict([k for k in sd if k.startswith("bit_estimator") or k.startswith("q_")])
         return self
 
+    # nn.Module calls test_video.py makes on the model (:301-302, :77)
+    def to(self, device):
+        return self
+
+    def eval(self):
+        return self
+
+    def parameters(self):
+        yield torch.empty(0, device=self.dev)
+
     def update(self, force=False):
         if self.entropy_coder is not None and not force:
             return
@@ -154,4 +164,4 @@ class IntraNoAR:
         bit = filesize(output_path) * 8
         height, width, q_in_ckpt, q_index, bit_stream = decode_i(output_path)
         dec = self.decompress(bit_stream, height, width, q_in_ckpt, q_index)
-        return {"bit": bit, "x_hat": dec["x_hat"]}
+        return {"bit": bit, "x_hat": dec["x_hat"].nchw_view()}

@@ -25,9 +25,21 @@ G1, G2, G4, G8, G16 = 48, 64, 96, 96, 128  # video_model.py:19-23
 
 
 def as_act(x, dtype=F32):
+    """Act view of a frame / DPB entry.  A (1, C, H, W) tensor that is the NCHW
+    view of a contiguous NHWC buffer (Act.nchw_view, what encode_decode hands
+    back to the harness) is wrapped without a copy; other tensors are copied
+    into a fresh NHWC buffer."""
     if isinstance(x, K.Act):
         return x
+    if x.dim() == 4 and x.shape[0] == 1 and x.is_cuda and x.dtype == K._TORCH[dtype]:
+        hwc = x[0].permute(1, 2, 0)
+        if hwc.is_contiguous():
+            return K.Act(hwc)
     return K.from_nchw(x, dtype)
+
+
+def dpb_in(dpb):
+    return {k: (as_act(v) if isinstance(v, torch.Tensor) else v) for k, v in dpb.items()}
 
 
 class DMC:
@@ -124,6 +136,16 @@ class DMC:
         if strict:
             ctx.check_strict([k for k in sd if k.startswith("bit_estimator") or "_q_" in k])
         return self
+
+    # nn.Module calls test_video.py makes on the model (:301-302, :77)
+    def to(self, device):
+        return self
+
+    def eval(self):
+        return self
+
+    def parameters(self):
+        yield torch.empty(0, device=self.dev)
 
     def update(self, force=False):
         """CompressionModel.update (common_model.py:63-68)."""
@@ -284,6 +306,7 @@ class DMC:
         (the encoder-side reconstruction is not computed: write mode returns
         the decoder's dpb, which is bit-identical)."""
         x = as_act(x)
+        dpb = dpb_in(dpb)
         mv_q_enc, mv_q_dec, y_q_enc, y_q_dec = self.get_q_for_inference(q_in_ckpt, q_index)
         dev = self.dev
         est_mv = self.optic_flow(x, dpb["ref_frame"])
@@ -323,6 +346,7 @@ class DMC:
     def decompress(self, dpb, string, height, width, q_in_ckpt, q_index, frame_idx):
         """video_model.py:483-520."""
         _, mv_q_dec, _, y_q_dec = self.get_q_for_inference(q_in_ckpt, q_index)
+        dpb = dpb_in(dpb)
         ec, dev = self.entropy_coder, self.dev
         ec.set_stream(string)
         zh, zw = get_downsampled_shape(height, width, 64)
@@ -346,7 +370,7 @@ class DMC:
         params = self._res_prior_params(z_hat, dpb, c3, yh, yw)
         y_hat = self.y_prior.decode(params, dec, self.scale_table)
         x_hat, feature = self._recon(y_hat, c1, c2, c3, y_q_dec)
-        return {"dpb": {"ref_frame": x_hat, "ref_feature": feature, "ref_mv_feature": mv_feature,
+        return {"dpb": {"ref_frame": x_hat.nchw_view(), "ref_feature": feature, "ref_mv_feature": mv_feature,
                         "ref_y": y_hat, "ref_mv_y": mv_y_hat}}
 
     def encode_decode(self, x, dpb, q_in_ckpt, q_index, output_path=None, pic_width=None, pic_height=None,

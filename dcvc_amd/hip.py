@@ -53,6 +53,7 @@ HIP_SYMBOLS = [
     ("dcvc_conv_pack_weights", ctypes.c_int64, [_vp, _i, _i, _i, _i, _i, _vp]),
     ("dcvc_conv2d", _i, [ctypes.POINTER(CConvArgs), _vp]),
     ("dcvc_set_option", _i, [ctypes.c_char_p, _i]),
+    ("dcvc_last_kernel", ctypes.c_char_p, []),
     ("dcvc_depthconv_block", _i, [ctypes.POINTER(CDcbArgs), _vp]),
     ("dcvc_dwconv3x3", _i, [_T, _T, _vp, _vp, _vp]),
     ("dcvc_flow_warp", _i, [_T, _T, _T, _vp, _vp, _vp]),
@@ -148,6 +149,12 @@ class Act:
     def nchw(self):
         return self.t().permute(2, 0, 1).unsqueeze(0).float()
 
+    def nchw_view(self):
+        """(1, C, H, W) torch view of the same memory (no copy): what the
+        reference harness receives as x_hat / dpb["ref_frame"]; in-place ops
+        on it (test_video.py's clamp_) act on this buffer."""
+        return self.t().permute(2, 0, 1).unsqueeze(0)
+
 
 NULL_T = CTensor(None, 0, 0, 0, 0, 0, 0)
 
@@ -225,7 +232,8 @@ def conv(cw, x, y=None, *, out_dtype=None, in_op=IN_NONE, in_slope=0.0, act=ACT_
         flops = 2 * Ho * Wo * cw.cout * cw.cin * cw.kh * cw.kw
         nb = (x.H * x.W * x.C * _esz(x.dtype) + cw.w.numel() * cw.w.element_size()
               + y.H * y.W * y.C * _esz(y.dtype) * (1 + (res is not None) + (res2 is not None)))
-        _t1(e0, "conv", flops, nb, f"k{cw.kh}s{cw.stride} {cw.cin}->{cw.cout} {x.H}x{x.W} "
+        kname = lib().dcvc_last_kernel().decode()
+        _t1(e0, kname.split("<")[0], flops, nb, f"{kname} | k{cw.kh}s{cw.stride} {cw.cin}->{cw.cout} {x.H}x{x.W} "
             f"{'bf16' if cw.compute == BF16 else 'f32'} in{x.dtype}out{y.dtype}{' shuf' if shuffle else ''}")
     return y
 
@@ -259,7 +267,8 @@ def depthconv_block(blk, x, y, scale=None):
         n = x.H * x.W
         fl = 2 * n * (a.cin * a.cin + 9 * a.cin + a.cin * a.cout * (2 if blk.adaptor is not None else 1)
                       + a.cout * hid * (3 if blk.gated else 2))
-        _t1(e0, "dcb_fused", fl, n * (a.cin + a.cout) * 2, f"dcb {a.cin}->{a.cout} {x.H}x{x.W}")
+        kname = lib().dcvc_last_kernel().decode()
+        _t1(e0, kname.split("<")[0], fl, n * (a.cin + a.cout) * 2, f"{kname} | dcb {a.cin}->{a.cout} {x.H}x{x.W}")
     return y
 
 

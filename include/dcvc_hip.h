@@ -96,6 +96,12 @@ int dcvc_conv2d(const dcvc_conv_args *a, void *stream);
  * "conv3x3_resident" = 1 (default) prefers its persistent resident-weight
  * variant where the weights fit in LDS. */
 int dcvc_set_option(const char *name, int value);
+/* Kernel instantiation launched by the last dcvc_conv2d / dcvc_depthconv_block
+ * call on the calling host thread, spelled as rocprofv3 reports it, with the
+ * grid size in work-items (e.g. "conv3x3_kernel<48, 16, false, unsigned
+ * short>@2088960"); "" before any launch.  Used to match per-launch HIP-event
+ * timings with rocprof kernel and PMC summaries. */
+const char *dcvc_last_kernel(void);
 
 /*
  * Fused DepthConvBlock (DepthConv + ConvFFN) / DepthConvBlock2 (+ ConvFFN2),

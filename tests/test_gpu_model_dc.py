@@ -90,7 +90,9 @@ def run_product(dc_golden, tag, prec):
             tr = net.entropy_coder.trace
             enc = [e for e in tr if e[0] == "enc"]
             dec = [e for e in tr if e[0] == "dec"]
-            rec = dpb["ref_frame"].nchw().cpu()[:, :, :h, :w]
+            # test_video.py:169-170: in-place clamp of the DPB frame, then crop
+            recon = dpb["ref_frame"].clamp_(0, 1)
+            rec = torch.nn.functional.pad(recon, (0, -(recon.shape[3] - w), 0, -(recon.shape[2] - h))).cpu()
             out.append({"enc": enc, "dec": dec, "bits": r["bit"], "psnr": psnr(rec, x), "recon": rec})
     return out
 
