@@ -39,7 +39,7 @@ def parse():
     ap.add_argument("--gop", type=int, default=32)
     ap.add_argument("--q_index", type=int, default=0)
     ap.add_argument("--precision", choices=["fast", "parity"], default="fast")
-    ap.add_argument("--stream_part", type=int, default=4,
+    ap.add_argument("--stream_part", type=int, default=8,
                     help="rANS stream parts (the reference's --stream_part_i/p); parts code in parallel threads")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")

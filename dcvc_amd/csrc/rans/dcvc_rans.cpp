@@ -5,11 +5,17 @@
 // so that streams are byte-identical; the implementation is organised for
 // throughput instead:
 //   * a CDF table is uploaded once (dcvc_cdf_table) instead of being copied on
-//     every call, and carries a 2^LUT_BITS-entry lookup per distribution so the
-//     decoder finds a symbol in O(1) instead of the reference's linear
-//     std::find_if over the CDF (rans.cpp:295-298);
-//   * symbols are resolved to (start, freq) pairs at encode time into one flat
-//     buffer per stream part, flushed in reverse in a single tight loop;
+//     every call.  It carries, per (row, symbol), the encoder's reciprocal
+//     step (ryg_rans' Rans64EncSymbol construction: x / f becomes a 64x64
+//     mul-high and a shift, exact for every x < 2^64) and, per row, a
+//     2^LUT_BITS-entry lookup so the decoder finds a symbol in O(1) instead of
+//     the reference's linear std::find_if over the CDF (rans.cpp:295-298);
+//   * encode calls only copy + validate their slice of symbols (in parallel,
+//     one task per stream part); flush walks every part's symbols last to
+//     first and resolves CDF entries and bypass escapes inline, so no
+//     intermediate step list is built;
+//   * stream parts are encoded and decoded on a persistent thread pool (one
+//     task per part) instead of a thread spawned per call;
 //   * every input is validated before any state changes; malformed streams
 //     stop with DCVC_ESTREAM instead of reading past the buffer.
 #include "../../../include/dcvc_rans.h"
@@ -19,12 +25,10 @@
 #include <cmath>
 #include <condition_variable>
 #include <cstring>
-#include <deque>
 #include <functional>
 #include <memory>
 #include <mutex>
 #include <new>
-#include <numeric>
 #include <thread>
 #include <vector>
 
@@ -34,16 +38,31 @@ constexpr uint32_t kPrecision = 16;             // probability bits (rans.cpp:27
 constexpr uint64_t kRansL = 1ull << 31;         // rANS64 lower bound
 constexpr uint32_t kBypassBits = 4;             // rans.cpp:29
 constexpr uint32_t kBypassMax = (1u << kBypassBits) - 1;
-constexpr int kLutBits = 10;
+constexpr int kLutBits = 7;
 constexpr uint32_t kMaxRawBypass = 1u << 28;    // keeps the bypass loop defined
+constexpr int kMaxStepsPerSymbol = 12;          // 1 + count steps + 7 pieces, rounded up
 
 // ---------------------------------------------------------------- tables
+struct EncStep {        // one precomputed rANS encode step (start, freq)
+  uint64_t rcp;         // reciprocal of freq (mul-high operand)
+  uint32_t bias;        // start, or start + 2^16 - 1 when freq == 1
+  uint16_t freq;
+  uint8_t shift;
+  uint8_t pad;
+};
+
+struct Row {
+  int32_t offset;       // symbol offset
+  int32_t maxv;         // cdf_size - 2: the escape symbol
+};
+
 struct CdfTable {
   int num = 0;
   int stride = 0;
-  std::vector<int32_t> cdf;      // [num][stride]
-  std::vector<int32_t> size;     // valid entries per row
-  std::vector<int32_t> offset;   // symbol offset per row
+  std::vector<int32_t> cdf;      // [num][stride], the caller's table
+  std::vector<Row> row;          // [num]
+  std::vector<uint32_t> packed;  // [num][stride] cdf[s] | (cdf[s+1]-cdf[s]) << 16
+  std::vector<EncStep> enc;      // [num][stride]
   std::vector<uint16_t> lut;     // [num][1 << kLutBits] first candidate symbol
 
   bool build(const int32_t *cdfs, int n, int st, const int32_t *sizes,
@@ -52,13 +71,45 @@ struct CdfTable {
     num = n;
     stride = st;
     cdf.assign(cdfs, cdfs + (size_t)n * st);
-    size.assign(sizes, sizes + n);
-    offset.assign(offs, offs + n);
+    row.resize(n);
+    packed.assign((size_t)n * st, 0);
+    enc.assign((size_t)n * st, EncStep{});
     lut.assign((size_t)n << kLutBits, 0);
     for (int t = 0; t < n; ++t) {
-      const int sz = size[t];
+      const int sz = sizes[t];
       if (sz < 2 || sz > st || sz > 65535) return false;
+      row[t] = {offs[t], sz - 2};
       const int32_t *c = &cdf[(size_t)t * st];
+      for (int s = 0; s + 1 < sz; ++s) {
+        const int64_t start = c[s], freq = (int64_t)c[s + 1] - c[s];
+        // a step the coder can take: 0 <= start, 0 < freq, start + freq <= 2^16
+        if (start < 0 || freq <= 0 || start + freq > (1 << kPrecision) || freq >= (1 << kPrecision)) {
+          // The reference accepts any table and misbehaves on such a step at
+          // coding time; here the step is marked unusable (freq 0) and
+          // coding a symbol that needs it fails with DCVC_EINVAL.
+          enc[(size_t)t * st + s] = EncStep{0, 0, 0, 0, 0};
+          packed[(size_t)t * st + s] = (uint32_t)(start & 0xffff);
+          continue;
+        }
+        packed[(size_t)t * st + s] = (uint32_t)start | ((uint32_t)freq << 16);
+        EncStep &e = enc[(size_t)t * st + s];
+        e.freq = (uint16_t)freq;
+        if (freq < 2) {
+          e.rcp = ~0ull;
+          e.shift = 0;
+          e.bias = (uint32_t)(start + (1 << kPrecision) - 1);
+        } else {
+          uint32_t shift = 0;
+          while ((uint64_t)freq > (1ull << shift)) ++shift;
+          uint64_t x0 = (uint64_t)freq - 1, x1 = 1ull << (shift + 31);
+          const uint64_t t1 = x1 / (uint64_t)freq;
+          x0 += (x1 % (uint64_t)freq) << 32;
+          const uint64_t t0 = x0 / (uint64_t)freq;
+          e.rcp = t0 + (t1 << 32);
+          e.shift = (uint8_t)(shift - 1);
+          e.bias = (uint32_t)start;
+        }
+      }
       uint16_t *l = &lut[(size_t)t << kLutBits];
       int s = 0;
       for (uint32_t b = 0; b < (1u << kLutBits); ++b) {
@@ -71,141 +122,208 @@ struct CdfTable {
   }
 };
 
-// ---------------------------------------------------------------- symbols
-struct Sym {            // one rANS step, mirrors RansSymbol (rans.h:36-40)
-  uint16_t start;
-  uint16_t range;
-  uint8_t bypass;
-};
-
-// Resolve one (symbol, index) pair into rANS steps (rans.cpp:90-137).
-// Returns DCVC_OK or DCVC_ERANGE; `out` is appended to.
-inline int push_symbol(std::vector<Sym> &out, const CdfTable &t, int idx,
-                       int64_t sym) {
-  const int32_t *c = &t.cdf[(size_t)idx * t.stride];
-  const int32_t max_value = t.size[idx] - 2;
-  int64_t value = sym - (int64_t)t.offset[idx];
-  uint64_t raw = 0;
-  if (value < 0) {
-    raw = (uint64_t)(-2 * value - 1);
-    value = max_value;
-  } else if (value >= max_value) {
-    raw = (uint64_t)(2 * (value - max_value));
-    value = max_value;
-  }
-  if (raw >= kMaxRawBypass) return DCVC_ERANGE;
-  out.push_back({(uint16_t)c[value], (uint16_t)(c[value + 1] - c[value]), 0});
-  if (value == max_value) {
-    uint32_t nb = 0;
-    while ((raw >> (nb * kBypassBits)) != 0) ++nb;
-    uint32_t v = nb;
-    while (v >= kBypassMax) {
-      out.push_back({(uint16_t)kBypassMax, (uint16_t)(kBypassMax + 1), 1});
-      v -= kBypassMax;
-    }
-    out.push_back({(uint16_t)v, (uint16_t)(v + 1), 1});
-    for (uint32_t j = 0; j < nb; ++j) {
-      const uint32_t piece = (uint32_t)(raw >> (j * kBypassBits)) & kBypassMax;
-      out.push_back({(uint16_t)piece, (uint16_t)(piece + 1), 1});
-    }
-  }
-  return DCVC_OK;
-}
-
-// rANS64 encode of the buffered steps, last step first (rans.cpp:141-168).
-bool flush_syms(const std::vector<Sym> &syms, std::vector<uint8_t> &stream) {
-  std::vector<uint32_t> words(syms.size() + 2);
-  uint32_t *end = words.data() + words.size();
-  uint32_t *p = end;
-  uint64_t x = kRansL;
-  for (size_t i = syms.size(); i-- > 0;) {
-    const Sym &s = syms[i];
-    if (!s.bypass) {
-      const uint64_t f = s.range;
-      if (f == 0) return false;
-      if (x >= ((kRansL >> kPrecision) << 32) * f) {
-        *--p = (uint32_t)x;
-        x >>= 32;
-      }
-      const uint64_t q = x / f;
-      x = (q << kPrecision) + (x - q * f) + s.start;
-    } else {
-      // Rans64EncPutBits (rans.cpp:37-55): freq = 2^(16-nbits)
-      const uint64_t f = 1ull << (kPrecision - kBypassBits);
-      if (x >= ((kRansL >> kPrecision) << 32) * f) {
-        *--p = (uint32_t)x;
-        x >>= 32;
-      }
-      x = (x << kBypassBits) | s.start;
-    }
-  }
-  p -= 2;  // Rans64EncFlush
-  p[0] = (uint32_t)x;
-  p[1] = (uint32_t)(x >> 32);
-  const size_t nbytes = (size_t)(end - p) * 4;
-  stream.resize(nbytes);
-  std::memcpy(stream.data(), p, nbytes);
-  return true;
-}
-
-// ---------------------------------------------------------------- worker
-class Worker {
+// ---------------------------------------------------------------- pool
+// Runs fn(0..tasks-1) on the calling thread plus `workers` persistent threads
+// and returns when every task is done.  Task indices are claimed with a CAS
+// on (generation << 32 | next), so a worker that wakes late can never run a
+// task of a later batch with an earlier batch's function.
+class Pool {
  public:
-  Worker() : th_([this] { loop(); }) {}
-  ~Worker() {
+  explicit Pool(int workers) {
+    for (int i = 0; i < workers; ++i) th_.emplace_back([this] { loop(); });
+  }
+  ~Pool() {
     {
       std::lock_guard<std::mutex> lk(mu_);
       stop_ = true;
     }
     cv_.notify_all();
-    th_.join();
+    for (auto &t : th_) t.join();
   }
-  void submit(std::function<void()> f) {
+  void run(int tasks, const std::function<void(int)> &fn) {
+    if (tasks <= 0) return;
+    if (th_.empty() || tasks == 1) {
+      for (int i = 0; i < tasks; ++i) fn(i);
+      return;
+    }
+    uint32_t gen;
     {
       std::lock_guard<std::mutex> lk(mu_);
-      q_.push_back(std::move(f));
-      ++pending_;
+      gen = ++gen_;
+      fn_ = &fn;
+      tasks_ = tasks;
+      remaining_ = tasks;
+      next_.store((uint64_t)gen << 32, std::memory_order_release);
     }
     cv_.notify_all();
-  }
-  void wait_idle() {
+    work(gen, fn, tasks);
     std::unique_lock<std::mutex> lk(mu_);
-    done_cv_.wait(lk, [this] { return pending_ == 0; });
+    done_.wait(lk, [this] { return remaining_ == 0; });
+    fn_ = nullptr;
   }
 
  private:
-  void loop() {
+  bool claim(uint32_t gen, int tasks, int *idx) {
+    uint64_t v = next_.load(std::memory_order_acquire);
     for (;;) {
-      std::function<void()> f;
-      {
-        std::unique_lock<std::mutex> lk(mu_);
-        cv_.wait(lk, [this] { return stop_ || !q_.empty(); });
-        if (q_.empty()) return;
-        f = std::move(q_.front());
-        q_.pop_front();
+      if ((uint32_t)(v >> 32) != gen || (int)(uint32_t)v >= tasks) return false;
+      if (next_.compare_exchange_weak(v, v + 1, std::memory_order_acq_rel)) {
+        *idx = (int)(uint32_t)v;
+        return true;
       }
-      f();
-      {
-        std::lock_guard<std::mutex> lk(mu_);
-        --pending_;
-      }
-      done_cv_.notify_all();
     }
   }
+  void work(uint32_t gen, const std::function<void(int)> &fn, int tasks) {
+    int i, n = 0;
+    while (claim(gen, tasks, &i)) {
+      fn(i);
+      ++n;
+    }
+    if (n) {
+      std::lock_guard<std::mutex> lk(mu_);
+      remaining_ -= n;
+      if (remaining_ == 0) done_.notify_all();
+    }
+  }
+  void loop() {
+    uint32_t seen = 0;
+    for (;;) {
+      const std::function<void(int)> *fn;
+      uint32_t gen;
+      int tasks;
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return stop_ || (gen_ != seen && fn_ != nullptr); });
+        if (stop_) return;
+        seen = gen = gen_;
+        fn = fn_;
+        tasks = tasks_;
+      }
+      work(gen, *fn, tasks);
+    }
+  }
+  std::vector<std::thread> th_;
   std::mutex mu_;
-  std::condition_variable cv_, done_cv_;
-  std::deque<std::function<void()>> q_;
-  int pending_ = 0;
+  std::condition_variable cv_, done_;
+  std::atomic<uint64_t> next_{0};
+  const std::function<void(int)> *fn_ = nullptr;
+  uint32_t gen_ = 0;
+  int tasks_ = 0;
+  int remaining_ = 0;
   bool stop_ = false;
-  std::thread th_;
+};
+
+// ---------------------------------------------------------------- encoder
+struct Record {                      // one encode call's slice of a part
+  std::shared_ptr<CdfTable> tab;
+  size_t off, n;
 };
 
 struct EncPart {
-  std::vector<Sym> syms;
-  std::vector<uint8_t> stream;
+  std::vector<int32_t> sym, idx;     // every buffered symbol / index, call order
+  std::vector<Record> rec;
+  std::unique_ptr<uint32_t[]> words; // flush output, written downwards
+  size_t cap = 0;
+  size_t begin = 0;                  // stream = words[begin, cap)
   int status = DCVC_OK;
   bool flushed = false;
 };
+
+inline uint64_t mulhi64(uint64_t a, uint64_t b) {
+  return (uint64_t)(((unsigned __int128)a * b) >> 64);
+}
+
+// rANS64 encode of one part, last symbol first (rans.cpp:141-168 on the step
+// list rans.cpp:90-137 would have built).  Bypass escapes of a symbol are
+// taken in reverse: raw pieces high to low, then the count steps, then the
+// symbol's own escape step.
+int flush_part(EncPart &p) {
+  size_t bound = 2;
+  for (const Record &r : p.rec) bound += r.n * kMaxStepsPerSymbol;
+  if (bound > p.cap) {
+    p.words.reset(new (std::nothrow) uint32_t[bound]);
+    if (!p.words) {
+      p.cap = 0;
+      return DCVC_ENOMEM;
+    }
+    p.cap = bound;
+  }
+  uint32_t *const end = p.words.get() + p.cap;
+  uint32_t *o = end;
+  uint64_t x = kRansL;
+  constexpr uint64_t kXmaxUnit = (kRansL >> kPrecision) << 32;
+  auto put_bits = [&](uint32_t v) {
+    if (x >= (kXmaxUnit << (kPrecision - kBypassBits))) {
+      *--o = (uint32_t)x;
+      x >>= 32;
+    }
+    x = (x << kBypassBits) | v;
+  };
+  for (size_t ri = p.rec.size(); ri-- > 0;) {
+    const Record &r = p.rec[ri];
+    const CdfTable &t = *r.tab;
+    const int32_t *sym = p.sym.data() + r.off;
+    const int32_t *idx = p.idx.data() + r.off;
+    const Row *rows = t.row.data();
+    const EncStep *steps = t.enc.data();
+    const size_t st = (size_t)t.stride;
+    for (size_t i = r.n; i-- > 0;) {
+      const int k = idx[i];
+      if (k < 0) continue;  // DC skip (rans.cpp:91-93)
+      const Row rw = rows[k];
+      int64_t value = (int64_t)sym[i] - rw.offset;
+      if (value < 0 || value >= rw.maxv) {
+        const uint64_t raw = value < 0 ? (uint64_t)(-2 * value - 1) : (uint64_t)(2 * (value - rw.maxv));
+        uint32_t nb = 0;
+        while ((raw >> (nb * kBypassBits)) != 0) ++nb;
+        for (uint32_t j = nb; j-- > 0;) put_bits((uint32_t)(raw >> (j * kBypassBits)) & kBypassMax);
+        put_bits(nb % kBypassMax);
+        for (uint32_t c = nb / kBypassMax; c-- > 0;) put_bits(kBypassMax);
+        value = rw.maxv;
+      }
+      const EncStep &e = steps[(size_t)k * st + (size_t)value];
+      if (e.freq == 0) return DCVC_EINVAL;
+      if (x >= kXmaxUnit * e.freq) {
+        *--o = (uint32_t)x;
+        x >>= 32;
+      }
+      const uint64_t q = mulhi64(x, e.rcp) >> e.shift;
+      x += e.bias + q * ((1u << kPrecision) - e.freq);
+    }
+  }
+  o -= 2;  // Rans64EncFlush
+  o[0] = (uint32_t)x;
+  o[1] = (uint32_t)(x >> 32);
+  p.begin = (size_t)(o - p.words.get());
+  return DCVC_OK;
+}
+
+// Copy + validate one part's slice of an encode call.
+template <typename T>
+int copy_slice(EncPart &p, const T *sym, const T *idx, size_t n, const CdfTable &t, bool dc) {
+  const size_t o = p.sym.size();
+  p.sym.resize(o + n);
+  p.idx.resize(o + n);
+  int32_t *ds = p.sym.data() + o, *di = p.idx.data() + o;
+  const int num = t.num;
+  for (size_t i = 0; i < n; ++i) {
+    const int32_t k = (int32_t)idx[i];
+    if (k >= num || (k < 0 && !dc)) return DCVC_EINVAL;
+    ds[i] = (int32_t)sym[i];
+    di[i] = k;
+  }
+  if (!dc) {
+    // HEM symbols: reject values the bypass coder cannot represent up front
+    // (the reference's bypass loop does not terminate on them)
+    for (size_t i = 0; i < n; ++i) {
+      const Row rw = t.row[di[i]];
+      const int64_t v = (int64_t)ds[i] - rw.offset;
+      const int64_t raw = v < 0 ? -2 * v - 1 : (v >= rw.maxv ? 2 * (v - rw.maxv) : 0);
+      if (raw >= (int64_t)kMaxRawBypass) return DCVC_ERANGE;
+    }
+  }
+  return DCVC_OK;
+}
 
 }  // namespace
 
@@ -216,7 +334,8 @@ struct dcvc_cdf_table {
 struct dcvc_rans_enc {
   int parts = 1;
   std::vector<EncPart> part;
-  std::vector<std::unique_ptr<Worker>> workers;  // empty when synchronous
+  std::unique_ptr<Pool> pool;
+  int status = DCVC_OK;   // first failure of an encode call since reset
 };
 
 struct dcvc_rans_dec {
@@ -224,73 +343,39 @@ struct dcvc_rans_dec {
   std::vector<std::vector<uint32_t>> words;  // per part
   std::vector<size_t> pos;                   // next word to read
   std::vector<uint64_t> state;
+  std::unique_ptr<Pool> pool;
 };
 
 namespace {
 
 template <typename T>
-int validate_indexes(const T *idx, int64_t n, const CdfTable &t,
-                     bool allow_negative) {
-  for (int64_t i = 0; i < n; ++i) {
-    const int64_t v = idx[i];
-    if (v < 0) {
-      if (!allow_negative) return DCVC_EINVAL;
-      continue;
-    }
-    if (v >= t.num) return DCVC_EINVAL;
-  }
-  return DCVC_OK;
-}
-
-template <typename T>
-int encode_slice(EncPart &p, const T *sym, const T *idx, int64_t n,
-                 const CdfTable &t) {
-  p.syms.reserve(p.syms.size() + (size_t)n + (size_t)n / 8);
-  for (int64_t i = 0; i < n; ++i) {
-    const int k = (int)idx[i];
-    if (k < 0) continue;  // DC skip (rans.cpp:91-93)
-    const int r = push_symbol(p.syms, t, k, (int64_t)sym[i]);
-    if (r != DCVC_OK) return r;
-  }
-  return DCVC_OK;
-}
-
-template <typename T>
 int enc_encode(dcvc_rans_enc *e, const T *symbols, const T *indexes, int64_t n,
-               std::shared_ptr<CdfTable> tab, bool allow_negative) {
-  if (!e || n < 0 || !tab || (n > 0 && (!symbols || !indexes)))
-    return DCVC_EINVAL;
-  int r = validate_indexes(indexes, n, *tab, allow_negative);
-  if (r != DCVC_OK) return r;
-  if (!allow_negative) {
-    // HEM symbols: reject values the bypass coder cannot represent up front
-    for (int64_t i = 0; i < n; ++i) {
-      const CdfTable &t = *tab;
-      const int k = (int)indexes[i];
-      const int64_t v = (int64_t)symbols[i] - t.offset[k];
-      const int64_t mv = t.size[k] - 2;
-      const int64_t raw = v < 0 ? -2 * v - 1 : (v >= mv ? 2 * (v - mv) : 0);
-      if (raw >= (int64_t)kMaxRawBypass) return DCVC_ERANGE;
-    }
-  }
+               std::shared_ptr<CdfTable> tab, bool dc) {
+  if (!e || n < 0 || !tab || (n > 0 && (!symbols || !indexes))) return DCVC_EINVAL;
   const int parts = e->parts;
   const int64_t each = n / parts;
-  for (int i = 0; i < parts; ++i) {
+  std::vector<int> st(parts, DCVC_OK);
+  std::vector<size_t> before(parts);
+  for (int i = 0; i < parts; ++i) before[i] = e->part[i].sym.size();
+  e->pool->run(parts, [&](int i) {
     const int64_t off = i * each;
     const int64_t cnt = (i < parts - 1) ? each : n - each * (parts - 1);
-    EncPart &p = e->part[i];
-    p.flushed = false;
-    if (e->workers.empty()) {
-      r = encode_slice(p, symbols + off, indexes + off, cnt, *tab);
-      if (r != DCVC_OK) return r;
-    } else {
-      auto s = std::make_shared<std::vector<T>>(symbols + off, symbols + off + cnt);
-      auto x = std::make_shared<std::vector<T>>(indexes + off, indexes + off + cnt);
-      e->workers[i]->submit([&p, s, x, tab] {
-        if (p.status != DCVC_OK) return;
-        p.status = encode_slice(p, s->data(), x->data(), (int64_t)s->size(), *tab);
-      });
+    st[i] = copy_slice(e->part[i], symbols + off, indexes + off, (size_t)cnt, *tab, dc);
+  });
+  for (int i = 0; i < parts; ++i) {
+    if (st[i] != DCVC_OK) {
+      // all-or-nothing: drop this call's symbols from every part
+      for (int j = 0; j < parts; ++j) {
+        e->part[j].sym.resize(before[j]);
+        e->part[j].idx.resize(before[j]);
+      }
+      return st[i];
     }
+  }
+  for (int i = 0; i < parts; ++i) {
+    EncPart &p = e->part[i];
+    p.rec.push_back({tab, before[i], p.sym.size() - before[i]});
+    p.flushed = false;
   }
   return DCVC_OK;
 }
@@ -320,23 +405,30 @@ int decode_slice(dcvc_rans_dec *d, int part, const TI *idx, int64_t n,
     return w[pos++];
   };
   const uint32_t mask = (1u << kPrecision) - 1;
+  const int num = t.num;
+  const size_t st = (size_t)t.stride;
+  const Row *rows = t.row.data();
+  const uint32_t *packed = t.packed.data();
+  const uint16_t *lut = t.lut.data();
   for (int64_t i = 0; i < n; ++i) {
     const int k = (int)idx[i];
-    if (k < 0) {  // only reachable in DC format; reference reads offsets[-1]
-      out[i] = 0;
+    if (k < 0) {
+      if (!dc_format) return DCVC_EINVAL;
+      out[i] = 0;  // reference reads offsets[-1]; a skipped symbol decodes as 0
       continue;
     }
-    const int32_t *c = &t.cdf[(size_t)k * t.stride];
-    const int32_t max_value = t.size[k] - 2;
+    if (k >= num) return DCVC_EINVAL;
+    const uint32_t *c = packed + (size_t)k * st;
+    const Row rw = rows[k];
     const uint32_t cum = (uint32_t)(x & mask);
-    int s = t.lut[((size_t)k << kLutBits) + (cum >> (kPrecision - kLutBits))];
-    while (s < max_value && (uint32_t)c[s + 1] <= cum) ++s;
-    const uint64_t start = (uint32_t)c[s];
-    const uint64_t freq = (uint32_t)(c[s + 1] - c[s]);
+    int s = lut[((size_t)k << kLutBits) + (cum >> (kPrecision - kLutBits))];
+    while (s < rw.maxv && (c[s + 1] & 0xffff) <= cum) ++s;
+    const uint32_t e = c[s];
+    const uint64_t start = e & 0xffff, freq = e >> 16;
     x = freq * (x >> kPrecision) + (x & mask) - start;
     if (x < kRansL) x = (x << 32) | next_word();
     int64_t value = s;
-    if (value == max_value) {
+    if (value == rw.maxv) {
       auto get_bits = [&]() -> uint32_t {
         const uint32_t v = (uint32_t)(x & kBypassMax);
         x >>= kBypassBits;
@@ -357,10 +449,10 @@ int decode_slice(dcvc_rans_dec *d, int part, const TI *idx, int64_t n,
       if (raw & 1)
         value = -value - 1;
       else
-        value += max_value;
+        value += rw.maxv;
     }
     if (bad) return DCVC_ESTREAM;
-    const int64_t res = value + t.offset[k];
+    const int64_t res = value + rw.offset;
     out[i] = dc_format ? (TO)(int16_t)res : (TO)res;
   }
   d->pos[part] = pos;
@@ -373,21 +465,20 @@ int dec_decode(dcvc_rans_dec *d, const TI *indexes, int64_t n,
                const CdfTable &t, TO *out, bool dc_format) {
   if (!d || n < 0 || (n > 0 && (!indexes || !out))) return DCVC_EINVAL;
   if (d->words.empty()) return DCVC_EINVAL;
-  int r = validate_indexes(indexes, n, t, dc_format);
-  if (r != DCVC_OK) return r;
+  // indexes are checked up front so a bad call leaves the decoder untouched
+  for (int64_t i = 0; i < n; ++i) {
+    const int64_t v = indexes[i];
+    if (v >= t.num || (v < 0 && !dc_format)) return DCVC_EINVAL;
+  }
   const int parts = d->parts;
   const int64_t each = n / parts;
   if (parts == 1) return decode_slice(d, 0, indexes, n, t, out, dc_format);
   std::vector<int> status(parts, DCVC_OK);
-  std::vector<std::thread> th;
-  for (int i = 0; i < parts; ++i) {
+  d->pool->run(parts, [&](int i) {
     const int64_t off = i * each;
     const int64_t cnt = (i < parts - 1) ? each : n - each * (parts - 1);
-    th.emplace_back([=, &status, &t] {
-      status[i] = decode_slice(d, i, indexes + off, cnt, t, out + off, dc_format);
-    });
-  }
-  for (auto &x : th) x.join();
+    status[i] = decode_slice(d, i, indexes + off, cnt, t, out + off, dc_format);
+  });
   for (int s : status)
     if (s != DCVC_OK) return s;
   return DCVC_OK;
@@ -469,9 +560,10 @@ dcvc_rans_enc *dcvc_rans_enc_create(int multithread, int stream_part) {
   e->parts = stream_part;
   e->part.resize(stream_part);
   // reference: multiThread || streamPart > 1 selects the threaded encoder
-  if (multithread || stream_part > 1)
-    for (int i = 0; i < stream_part; ++i)
-      e->workers.emplace_back(new Worker());
+  // (py_rans.cpp:11-20); here the parts are worked on by a pool of
+  // stream_part - 1 threads plus the caller.  The stream is the same either way.
+  (void)multithread;
+  e->pool.reset(new Pool(stream_part - 1));
   return e;
 }
 
@@ -505,27 +597,17 @@ int dcvc_rans_enc_encode_table_i32(dcvc_rans_enc *e, const int32_t *symbols,
 
 int dcvc_rans_enc_flush(dcvc_rans_enc *e) {
   if (!e) return DCVC_EINVAL;
-  for (int i = 0; i < e->parts; ++i) {
+  e->pool->run(e->parts, [e](int i) {
     EncPart &p = e->part[i];
-    auto job = [&p] {
-      if (p.status == DCVC_OK && !flush_syms(p.syms, p.stream))
-        p.status = DCVC_EINVAL;
-      p.flushed = true;
-    };
-    if (e->workers.empty())
-      job();
-    else
-      e->workers[i]->submit(job);
-  }
-  if (e->workers.empty()) {
-    for (auto &p : e->part)
-      if (p.status != DCVC_OK) return p.status;
-  }
+    p.status = flush_part(p);
+    p.flushed = true;
+  });
+  for (auto &p : e->part)
+    if (p.status != DCVC_OK) return p.status;
   return DCVC_OK;
 }
 
-static int enc_wait(dcvc_rans_enc *e) {
-  for (auto &w : e->workers) w->wait_idle();
+static int enc_ready(dcvc_rans_enc *e) {
   for (auto &p : e->part) {
     if (p.status != DCVC_OK) return p.status;
     if (!p.flushed) return DCVC_EBUSY;
@@ -533,21 +615,22 @@ static int enc_wait(dcvc_rans_enc *e) {
   return DCVC_OK;
 }
 
+static size_t part_bytes(const EncPart &p) { return (p.cap - p.begin) * 4; }
+
 static int header_bytes(const dcvc_rans_enc *e, int *per) {
   size_t maxsz = 0;
-  for (int i = 0; i + 1 < e->parts; ++i)
-    maxsz = std::max(maxsz, e->part[i].stream.size());
+  for (int i = 0; i + 1 < e->parts; ++i) maxsz = std::max(maxsz, part_bytes(e->part[i]));
   *per = maxsz > 65535 ? 4 : 2;
   return 1 + (e->parts > 1 ? (e->parts - 1) * *per : 0);
 }
 
 int64_t dcvc_rans_enc_stream_size(dcvc_rans_enc *e, int with_header) {
   if (!e) return DCVC_EINVAL;
-  int r = enc_wait(e);
+  int r = enc_ready(e);
   if (r != DCVC_OK) return r;
   if (!with_header && e->parts != 1) return DCVC_EINVAL;
   int64_t total = 0;
-  for (auto &p : e->part) total += (int64_t)p.stream.size();
+  for (auto &p : e->part) total += (int64_t)part_bytes(p);
   if (with_header) {
     int per;
     total += header_bytes(e, &per);
@@ -566,23 +649,25 @@ int64_t dcvc_rans_enc_get_stream(dcvc_rans_enc *e, int with_header,
     const int hb = header_bytes(e, &per);
     o[0] = (uint8_t)(((e->parts - 1) << 4) + (per == 2 ? 1 : 0));
     for (int i = 0; i + 1 < e->parts; ++i) {
-      const uint32_t sz = (uint32_t)e->part[i].stream.size();
+      const uint32_t sz = (uint32_t)part_bytes(e->part[i]);
       for (int b = 0; b < per; ++b) o[1 + per * i + b] = (uint8_t)(sz >> (8 * b));
     }
     o += hb;
   }
   for (auto &p : e->part) {
-    std::memcpy(o, p.stream.data(), p.stream.size());
-    o += p.stream.size();
+    std::memcpy(o, p.words.get() + p.begin, part_bytes(p));
+    o += part_bytes(p);
   }
   return need;
 }
 
 int dcvc_rans_enc_reset(dcvc_rans_enc *e) {
   if (!e) return DCVC_EINVAL;
-  for (auto &w : e->workers) w->wait_idle();
   for (auto &p : e->part) {
-    p.syms.clear();
+    p.sym.clear();
+    p.idx.clear();
+    p.rec.clear();
+    p.begin = p.cap;
     p.status = DCVC_OK;
     p.flushed = false;
   }
@@ -594,6 +679,7 @@ dcvc_rans_dec *dcvc_rans_dec_create(int stream_part) {
   auto *d = new (std::nothrow) dcvc_rans_dec;
   if (!d) return nullptr;
   d->parts = stream_part;
+  d->pool.reset(new Pool(stream_part - 1));
   return d;
 }
 
