@@ -666,9 +666,15 @@ int pick_bn(const C3 &p, hipStream_t st) {
 // Called by dcvc_conv2d (after its argument validation) for 3x3 / stride 1 /
 // pad 1 convs with bf16 input and compute; DCVC_HIP_EUNSUPPORTED sends the
 // call to the generic kernel.
+extern "C" int dcvc_internal_conv3p(const dcvc_conv_args *a, void *stream);
+
 extern "C" int dcvc_internal_conv3x3(const dcvc_conv_args *a, void *stream) {
   if (a->kh != 3 || a->kw != 3 || a->stride != 1 || a->pad != 1 || a->compute != DCVC_BF16)
     return DCVC_HIP_EUNSUPPORTED;
+  {
+    const int r = dcvc_internal_conv3p(a, stream);  // persistent kernel (conv3x3p.hip) first
+    if (r != DCVC_HIP_EUNSUPPORTED) return r;
+  }
   if (a->x.dtype != DCVC_BF16 || (a->in_op != DCVC_IN_NONE && a->in_op != DCVC_IN_LRELU))
     return DCVC_HIP_EUNSUPPORTED;
   if (a->cin % 16 || a->x.cstride % 8 || a->x.coff % 8 || ((uintptr_t)a->x.ptr & 15))

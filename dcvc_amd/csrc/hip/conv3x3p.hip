@@ -1,0 +1,449 @@
+// Persistent 3x3 stride-1 convolution for bf16 NHWC feature maps with
+// 32..128 input channels and <= 64 output channels per workgroup: the
+// full-resolution ResBlock / context-fusion / recon convs of DCVC-DC
+// (SURVEY §8 a13-a15).
+//
+// Why a second 3x3 kernel: the per-workgroup kernel (conv3x3.hip) restages
+// the whole weight slice for every 16x16 tile and waits out one HBM round
+// trip per 32-channel chunk; rocprofv3 counted 49 % of its wave cycles in
+// s_waitcnt/barrier waits and ~13 VALU instructions per MFMA (epilogue and
+// staging generality), with the MFMA pipe 14 % busy (profiles/r01_*).
+// This kernel is organised around hiding that latency instead:
+//   * one 512-thread workgroup per CU (grid = #CUs x n-blocks) keeps its
+//     BN-channel weight slice resident in LDS for the whole launch and walks
+//     16x16 output tiles (8 waves x 2 pixel rows);
+//   * the next tile's input is loaded into registers right after the current
+//     tile's image is published, so its HBM latency hides behind the current
+//     tile's MFMAs and epilogue (software pipeline, prefetch distance 1);
+//   * a thread's staging pieces run along the channel axis first, so the
+//     threads of a wave read whole contiguous pixel rows (CIN * 2 bytes per
+//     pixel) instead of 64-byte pieces one pixel stride apart;
+//   * the tiles of one XCD's workgroups are consecutive in raster order, so
+//     halo rows and columns shared by neighbouring tiles are L2 hits;
+//   * the epilogue is specialised to what these layers need (bias, leaky
+//     ReLU, up to two bf16 residuals, per-channel scale, bf16 store) and
+//     goes through an fp32 LDS tile that reuses the input image's space.
+// The MFMA sequence (per 32-channel chunk, taps 0..8; then a 16-channel tail
+// as five tap pairs) and the fp32 epilogue order are those of conv3x3.hip, so
+// results are bit-identical to it (tests/test_gpu_kernels.py).
+#include "common.h"
+
+namespace {
+
+constexpr int kPitch = 20;  // LDS pixels per halo row (18 used)
+
+struct P3 {
+  const uint16_t *x;
+  int H, W, xcs, xco;
+  const uint16_t *w;  // packed [cout][3][3][cinp] bf16
+  int cinp;
+  const float *bias;
+  const float *scale;
+  uint16_t *y;
+  int ycs, yco;
+  const uint16_t *res;
+  int rcs, rco;
+  const uint16_t *res2;
+  int r2cs, r2co;
+  int cout;
+  int in_lrelu;
+  float in_slope;
+  int act;
+  float slope;
+  int tiles_x, tiles_y, nblk_n;
+  int xbytes, rbytes, r2bytes;
+};
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ int swz(int row, int x, int slot) {
+  return row * 32 + ((slot ^ (((x >> 2) & 1) << 1)) << 3);
+}
+
+template <int CIN, int BN, int NW, int RW>
+struct Geo {
+  static constexpr int NCH = CIN / 32;
+  static constexpr bool TAIL = (CIN % 32) == 16;
+  static constexpr int NIMG = NCH + (TAIL ? 1 : 0);
+  static constexpr int KS = 9 * NCH + (TAIL ? 5 : 0);
+  static constexpr int TH = NW * RW;
+  static constexpr int IH = TH + 2;
+  static constexpr int NT = BN / 16;
+  static constexpr int NTHR = NW * 64;
+  static constexpr int IMG = IH * kPitch * 32;            // elements per chunk image
+  static constexpr size_t WB = (size_t)KS * BN * 64;      // resident weights
+  static constexpr int LD = BN + 4;                       // fp32 epilogue tile row
+  static constexpr size_t TB = (size_t)TH * 16 * LD * 4;
+  static constexpr size_t IB = (size_t)NIMG * IMG * 2;
+  static constexpr size_t BUF = IB > TB ? IB : TB;
+  static constexpr size_t LC = WB + BUF;                  // bias | scale
+  static constexpr size_t LDS = LC + 2 * BN * 4;
+  static constexpr int QP = CIN / 8;                      // 16-byte pieces per pixel
+  static constexpr int PIX = IH * 18;
+  static constexpr int PP = (PIX * QP + NTHR - 1) / NTHR; // input pieces per thread
+  static constexpr int OQ = BN / 8;
+  static constexpr int PO = (TH * 16 * OQ + NTHR - 1) / NTHR;  // output pieces per thread
+};
+
+template <int CIN, int BN, int NW, int RW>
+__global__ void __launch_bounds__(NW * 64) conv3p_kernel(P3 p) {
+  typedef Geo<CIN, BN, NW, RW> G_;
+  constexpr int NCH = G_::NCH, KS = G_::KS, NT = G_::NT, TH = G_::TH, IMG = G_::IMG;
+  constexpr int NTHR = G_::NTHR, QP = G_::QP, PP = G_::PP, LD = G_::LD, OQ = G_::OQ, PO = G_::PO;
+  constexpr int ROWB = kPitch * 32;
+  extern __shared__ __align__(16) unsigned char smem[];
+  uint16_t *Lw = reinterpret_cast<uint16_t *>(smem);
+  uint16_t *Li = reinterpret_cast<uint16_t *>(smem + G_::WB);
+  float *T = reinterpret_cast<float *>(smem + G_::WB);
+  float *Lc = reinterpret_cast<float *>(smem + G_::LC);
+
+  const int tid = threadIdx.x;
+  const int wave = tid >> 6, lane = tid & 63;
+  const int col = lane & 15, hi = lane >> 4;
+  const int nb = blockIdx.x % p.nblk_n;
+  const int n0 = nb * BN;
+  const int G = gridDim.x / p.nblk_n;
+  int g = blockIdx.x / p.nblk_n;
+  // consecutive tiles on one XCD (workgroups are dealt to XCDs round robin)
+  if (p.nblk_n == 1 && (G & 7) == 0) g = (g & 7) * (G >> 3) + (g >> 3);
+  const int ntiles = p.tiles_x * p.tiles_y;
+  if (g >= ntiles) return;
+
+  // ---- per-thread staging plan: piece u = (halo pixel, 16-byte channel piece)
+  int lofs[PP], rel[PP], pyx[PP];
+#pragma unroll
+  for (int u = 0; u < PP; ++u) {
+    const int it = tid + u * NTHR;
+    lofs[u] = -1;
+    rel[u] = 0;
+    pyx[u] = 0;
+    if (it < G_::PIX * QP) {
+      const int pix = it / QP, q = it - pix * QP;
+      const int iy = pix / 18, ix = pix - iy * 18;
+      const int c = q >> 2, slot = q & 3;
+      lofs[u] = c * IMG + swz(iy * kPitch + ix, ix, slot);
+      rel[u] = ((iy - 1) * p.W + (ix - 1)) * p.xcs + p.xco + q * 8;
+      pyx[u] = (iy << 8) | ix;
+    }
+  }
+  // buffer loads: an out-of-range offset returns zeros, so halo pixels outside
+  // the image need no branch (a branch around each load makes hipcc wait for
+  // it on the spot, which would serialise the prefetch)
+  const __amdgpu_buffer_rsrc_t xr =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t *>(p.x), (short)0, p.xbytes, 0x00020000);
+  u16x8 pf[PP];
+  auto issue = [&](int t) {
+    const int oy0 = (t / p.tiles_x) * TH, ox0 = (t % p.tiles_x) * 16;
+    const int base = (oy0 * p.W + ox0) * p.xcs;
+#pragma unroll
+    for (int u = 0; u < PP; ++u) {
+      const int gy = oy0 - 1 + (pyx[u] >> 8), gx = ox0 - 1 + (pyx[u] & 255);
+      const bool in = lofs[u] >= 0 && gy >= 0 && gy < p.H && gx >= 0 && gx < p.W;
+      const int off = in ? (base + rel[u]) * 2 : 0x7ffffff0;
+      const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0);
+      pf[u] = __builtin_bit_cast(u16x8, v);
+    }
+  };
+  auto publish = [&]() {
+    if (p.in_lrelu) {
+#pragma unroll
+      for (int u = 0; u < PP; ++u) {
+        if (lofs[u] < 0) continue;
+        u16x8 v = pf[u];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float f = bf2f(v[j]);
+          v[j] = f2bf(f >= 0.f ? f : f * p.in_slope);
+        }
+        *reinterpret_cast<u16x8 *>(Li + lofs[u]) = v;
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < PP; ++u)
+        if (lofs[u] >= 0) *reinterpret_cast<u16x8 *>(Li + lofs[u]) = pf[u];
+    }
+  };
+
+  issue(g);
+  // ---- resident weights [KS][BN][32] (swizzled by row) + epilogue constants
+  for (int it = tid; it < KS * BN * 4; it += NTHR) {
+    const int row = it >> 2, sl = it & 3;
+    const int ks = row / BN, n = n0 + row - ks * BN;
+    int tap, c;
+    if (ks < 9 * NCH) {
+      tap = ks % 9;
+      c = (ks / 9) * 32 + sl * 8;
+    } else {
+      tap = 2 * (ks - 9 * NCH) + (sl >> 1);
+      c = NCH * 32 + (sl & 1) * 8;
+    }
+    u16x8 v;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = 0;
+    if (tap < 9 && n < p.cout) v = *reinterpret_cast<const u16x8 *>(p.w + ((int64_t)n * 9 + tap) * p.cinp + c);
+    *reinterpret_cast<u16x8 *>(Lw + swz(row, row, sl)) = v;
+  }
+  for (int i = tid; i < BN; i += NTHR) {
+    const int n = n0 + i;
+    Lc[i] = (p.bias && n < p.cout) ? p.bias[n] : 0.f;
+    Lc[BN + i] = (p.scale && n < p.cout) ? p.scale[n] : 1.f;
+  }
+
+  // per-lane MFMA operand bases (elements)
+  int offB[3];
+#pragma unroll
+  for (int dx = 0; dx < 3; ++dx) offB[dx] = swz(wave * RW * kPitch + col + dx, col + dx, hi);
+  int offT[5];
+#pragma unroll
+  for (int pr = 0; pr < 5; ++pr) {
+    int t = 2 * pr + (hi >> 1);
+    if (t > 8) t = 0;  // tap 9: zero weights, any finite data
+    const int dy = t / 3, dx = t - dy * 3;
+    offT[pr] = NCH * IMG + swz((wave * RW + dy) * kPitch + col + dx, col + dx, hi & 1);
+  }
+  const uint16_t *LwA = Lw + swz(col, col, hi);
+  const __amdgpu_buffer_rsrc_t rr =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t *>(p.res), (short)0, p.rbytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rr2 =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t *>(p.res2), (short)0, p.r2bytes, 0x00020000);
+
+  for (int t = g;;) {
+    publish();
+    __syncthreads();
+    const int tn = t + G;
+    const bool more = tn < ntiles;
+    if (more) issue(tn);  // in flight across this tile's MFMAs and epilogue
+
+    f32x4 acc[RW][NT];
+#pragma unroll
+    for (int r = 0; r < RW; ++r)
+#pragma unroll
+      for (int j = 0; j < NT; ++j) acc[r][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+#pragma unroll
+      for (int k = 0; k < 9; ++k) {
+        const int dy = k / 3, dx = k % 3;
+        bf16x8 a[NT], b[RW];
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+          a[j] = *reinterpret_cast<const bf16x8 *>(LwA + ((c * 9 + k) * BN + j * 16) * 32);
+#pragma unroll
+        for (int r = 0; r < RW; ++r)
+          b[r] = *reinterpret_cast<const bf16x8 *>(Li + c * IMG + offB[dx] + (r + dy) * ROWB);
+#pragma unroll
+        for (int r = 0; r < RW; ++r)
+#pragma unroll
+          for (int j = 0; j < NT; ++j)
+            acc[r][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[j], b[r], acc[r][j], 0, 0, 0);
+      }
+    }
+    if constexpr (G_::TAIL) {
+#pragma unroll
+      for (int pr = 0; pr < 5; ++pr) {
+        bf16x8 a[NT], b[RW];
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+          a[j] = *reinterpret_cast<const bf16x8 *>(LwA + ((9 * NCH + pr) * BN + j * 16) * 32);
+#pragma unroll
+        for (int r = 0; r < RW; ++r) b[r] = *reinterpret_cast<const bf16x8 *>(Li + offT[pr] + r * ROWB);
+#pragma unroll
+        for (int r = 0; r < RW; ++r)
+#pragma unroll
+          for (int j = 0; j < NT; ++j)
+            acc[r][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[j], b[r], acc[r][j], 0, 0, 0);
+      }
+    }
+    __syncthreads();  // every wave is done reading the image: T may overwrite it
+
+    // ---- epilogue A: v = act(acc + bias) -> fp32 tile T[pixel][LD]
+#pragma unroll
+    for (int r = 0; r < RW; ++r)
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+        const int nl = j * 16 + hi * 4;
+        const float4 b = *reinterpret_cast<const float4 *>(Lc + nl);
+        float4 o;
+        o.x = acc[r][j][0] + b.x;
+        o.y = acc[r][j][1] + b.y;
+        o.z = acc[r][j][2] + b.z;
+        o.w = acc[r][j][3] + b.w;
+        if (p.act == DCVC_ACT_LRELU) {
+          o.x = o.x >= 0.f ? o.x : o.x * p.slope;
+          o.y = o.y >= 0.f ? o.y : o.y * p.slope;
+          o.z = o.z >= 0.f ? o.z : o.z * p.slope;
+          o.w = o.w >= 0.f ? o.w : o.w * p.slope;
+        }
+        *reinterpret_cast<float4 *>(T + ((wave * RW + r) * 16 + col) * LD + nl) = o;
+      }
+    __syncthreads();
+
+    // ---- epilogue B: out = scale * (res2 + (res + v)), 16-byte bf16 pieces
+    {
+      const int oy0 = (t / p.tiles_x) * TH, ox0 = (t % p.tiles_x) * 16;
+      int64_t pix[PO];
+      int q8[PO];
+      bool ok[PO];
+      u16x8 r1[PO], r2[PO];
+#pragma unroll
+      for (int u = 0; u < PO; ++u) {
+        const int it = tid + u * NTHR;
+        const int l = it / OQ, q = it - (it / OQ) * OQ;
+        const int oy = oy0 + (l >> 4), ox = ox0 + (l & 15);
+        ok[u] = it < TH * 16 * OQ && oy < p.H && ox < p.W;
+        pix[u] = (int64_t)oy * p.W + ox;
+        q8[u] = q * 8;
+        if (p.res) {
+          const int off = ok[u] ? (int)(pix[u] * p.rcs + p.rco + n0 + q * 8) * 2 : 0x7ffffff0;
+          r1[u] = __builtin_bit_cast(u16x8, __builtin_amdgcn_raw_buffer_load_b128(rr, off, 0, 0));
+        }
+        if (p.res2) {
+          const int off = ok[u] ? (int)(pix[u] * p.r2cs + p.r2co + n0 + q * 8) * 2 : 0x7ffffff0;
+          r2[u] = __builtin_bit_cast(u16x8, __builtin_amdgcn_raw_buffer_load_b128(rr2, off, 0, 0));
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < PO; ++u) {
+        if (!ok[u]) continue;
+        const int it = tid + u * NTHR;
+        const int l = it / OQ;
+        const float4 a = *reinterpret_cast<const float4 *>(T + l * LD + q8[u]);
+        const float4 b = *reinterpret_cast<const float4 *>(T + l * LD + q8[u] + 4);
+        float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+        if (p.res) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[j] = bf2f(r1[u][j]) + v[j];
+        }
+        if (p.res2) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[j] = bf2f(r2[u][j]) + v[j];
+        }
+        if (p.scale) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[j] = v[j] * Lc[BN + q8[u] + j];
+        }
+        u16x8 o;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = f2bf(v[j]);
+        *reinterpret_cast<u16x8 *>(p.y + pix[u] * p.ycs + p.yco + n0 + q8[u]) = o;
+      }
+    }
+    if (!more) break;
+    __syncthreads();  // T read by every thread before the next image overwrites it
+    t = tn;
+  }
+}
+
+int g_cus = 0;
+int g_enabled = 1;
+
+template <int CIN, int BN, int NW, int RW>
+int launch(P3 p, hipStream_t st) {
+  typedef Geo<CIN, BN, NW, RW> G_;
+  if constexpr (G_::LDS > 160 * 1024) {
+    return DCVC_HIP_EUNSUPPORTED;
+  } else {
+    p.tiles_x = (p.W + 15) / 16;
+    p.tiles_y = (p.H + G_::TH - 1) / G_::TH;
+    p.nblk_n = (p.cout + BN - 1) / BN;
+    const int64_t ntiles = (int64_t)p.tiles_x * p.tiles_y;
+    if (g_cus <= 0) {
+      int dev = 0;
+      hipDeviceProp_t prop;
+      if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess)
+        return DCVC_HIP_ELAUNCH;
+      g_cus = prop.multiProcessorCount;
+    }
+    // a grid of fewer tiles than workgroups is better served per tile
+    if (ntiles < 2LL * g_cus) return DCVC_HIP_EUNSUPPORTED;
+    int64_t G = g_cus / p.nblk_n;
+    if (G < 8) G = 8;
+    auto kern = conv3p_kernel<CIN, BN, NW, RW>;
+    dcvc_note_kernel("conv3p_kernel<%d, %d, %d, %d>@%lld", CIN, BN, NW, RW, (long long)G * p.nblk_n * NW * 64);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)G_::LDS);
+    hipLaunchKernelGGL(kern, dim3((unsigned)(G * p.nblk_n)), dim3(NW * 64), G_::LDS, st, p);
+    DCVC_LAUNCH_CHECK();
+    return DCVC_HIP_OK;
+  }
+}
+
+// 16 output rows per tile (8 waves x 2) when the LDS holds it, else 8.
+template <int CIN, int BN>
+int pick_th(const P3 &p, hipStream_t st) {
+  if constexpr (Geo<CIN, BN, 8, 2>::LDS <= 160 * 1024) return launch<CIN, BN, 8, 2>(p, st);
+  return launch<CIN, BN, 8, 1>(p, st);
+}
+
+template <int CIN>
+int pick_bn(const P3 &p, hipStream_t st) {
+  if (p.cout % 64 == 0 && Geo<CIN, 64, 8, 1>::LDS <= 160 * 1024) return pick_th<CIN, 64>(p, st);
+  if (p.cout % 48 == 0) return pick_th<CIN, 48>(p, st);
+  if (p.cout % 32 == 0) return pick_th<CIN, 32>(p, st);
+  return DCVC_HIP_EUNSUPPORTED;
+}
+
+}  // namespace
+
+// Called by dcvc_internal_conv3x3 for bf16 -> bf16 3x3 stride-1 convs without
+// pixel shuffle; DCVC_HIP_EUNSUPPORTED hands the call on to conv3x3.hip.
+extern "C" int dcvc_internal_conv3p(const dcvc_conv_args *a, void *stream) {
+  if (!g_enabled) return DCVC_HIP_EUNSUPPORTED;
+  if (a->x.dtype != DCVC_BF16 || a->y.dtype != DCVC_BF16 || a->shuffle) return DCVC_HIP_EUNSUPPORTED;
+  if (a->act != DCVC_ACT_NONE && a->act != DCVC_ACT_LRELU) return DCVC_HIP_EUNSUPPORTED;
+  if (a->in_op != DCVC_IN_NONE && a->in_op != DCVC_IN_LRELU) return DCVC_HIP_EUNSUPPORTED;
+  if (a->x.cstride % 8 || a->x.coff % 8 || ((uintptr_t)a->x.ptr & 15)) return DCVC_HIP_EUNSUPPORTED;
+  if (a->y.cstride % 8 || a->y.coff % 8 || ((uintptr_t)a->y.ptr & 15) || a->cout % 8) return DCVC_HIP_EUNSUPPORTED;
+  if (a->res.ptr && (a->res.dtype != DCVC_BF16 || a->res.cstride % 8 || a->res.coff % 8 || ((uintptr_t)a->res.ptr & 15)))
+    return DCVC_HIP_EUNSUPPORTED;
+  if (a->res2.ptr &&
+      (a->res2.dtype != DCVC_BF16 || a->res2.cstride % 8 || a->res2.coff % 8 || ((uintptr_t)a->res2.ptr & 15)))
+    return DCVC_HIP_EUNSUPPORTED;
+  if ((int64_t)a->x.H * a->x.W * a->x.cstride >= ((int64_t)1 << 31) - 16) return DCVC_HIP_EUNSUPPORTED;
+  if ((int64_t)a->y.H * a->y.W * a->y.cstride >= ((int64_t)1 << 30) - 16) return DCVC_HIP_EUNSUPPORTED;
+  if ((int64_t)a->x.H * a->x.W * a->x.cstride >= ((int64_t)1 << 30) - 16) return DCVC_HIP_EUNSUPPORTED;
+  P3 p{};
+  p.x = reinterpret_cast<const uint16_t *>(a->x.ptr);
+  p.H = a->x.H;
+  p.W = a->x.W;
+  p.xcs = a->x.cstride;
+  p.xco = a->x.coff;
+  p.w = reinterpret_cast<const uint16_t *>(a->w);
+  p.cinp = (a->cin + 31) / 32 * 32;
+  p.bias = a->bias;
+  p.scale = a->scale;
+  p.y = reinterpret_cast<uint16_t *>(a->y.ptr);
+  p.ycs = a->y.cstride;
+  p.yco = a->y.coff;
+  if (a->res.ptr) {
+    p.res = reinterpret_cast<const uint16_t *>(a->res.ptr);
+    p.rcs = a->res.cstride;
+    p.rco = a->res.coff;
+  }
+  if (a->res2.ptr) {
+    p.res2 = reinterpret_cast<const uint16_t *>(a->res2.ptr);
+    p.r2cs = a->res2.cstride;
+    p.r2co = a->res2.coff;
+  }
+  p.xbytes = a->x.H * a->x.W * a->x.cstride * 2;
+  if (a->res.ptr) p.rbytes = a->res.H * a->res.W * a->res.cstride * 2;
+  if (a->res2.ptr) p.r2bytes = a->res2.H * a->res2.W * a->res2.cstride * 2;
+  p.cout = a->cout;
+  p.in_lrelu = a->in_op == DCVC_IN_LRELU;
+  p.in_slope = a->in_slope;
+  p.act = a->act;
+  p.slope = a->slope;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  switch (a->cin) {
+    case 32: return pick_bn<32>(p, st);
+    case 48: return pick_bn<48>(p, st);
+    case 64: return pick_bn<64>(p, st);
+    case 80: return pick_bn<80>(p, st);
+    case 96: return pick_bn<96>(p, st);
+    case 128: return pick_bn<128>(p, st);
+    default: return DCVC_HIP_EUNSUPPORTED;
+  }
+}
+
+// dcvc_set_option("conv3x3_persistent", 0/1) (A/B switch, via conv.hip)
+extern "C" void dcvc_internal_conv3p_enable(int v) { g_enabled = v; }

@@ -230,7 +230,10 @@ int launch(G1 p, hipStream_t st) {
 
 // Tile selection: BN is the 16-multiple tile (<= 128) that wastes the fewest
 // MFMA columns; BM is as large as the grid allows while keeping >= 512
-// workgroups (the 68x120 latent GEMMs need the small tiles to fill 256 CUs).
+// workgroups.  The 68x120 latent GEMMs (8160 pixels) are latency-bound at
+// one workgroup per CU: below 768 workgroups at BM = 64 they take BM = 32
+// (where a 2x2 wave layout exists), so each CU holds ~3 workgroups' loads in
+// flight.
 template <typename TIN, typename TOUT>
 int dispatch(const G1 &p, hipStream_t st) {
   static const int cand[6] = {16, 32, 48, 64, 96, 128};
@@ -247,15 +250,23 @@ int dispatch(const G1 &p, hipStream_t st) {
   auto blocks = [&](int bm) { return ((p.M + bm - 1) / bm) * tn; };
   const bool big = blocks(bn <= 64 ? 256 : 128) >= 512;
   const bool mid = blocks(128) >= 512;
+  const bool small = blocks(64) < 768;
   switch (bn) {
     case 16: return big ? launch<TIN, TOUT, 256, 16, 4>(p, st) : launch<TIN, TOUT, 64, 16, 4>(p, st);
-    case 32: return big ? launch<TIN, TOUT, 256, 32, 4>(p, st) : launch<TIN, TOUT, 64, 32, 4>(p, st);
+    case 32:
+      if (big) return launch<TIN, TOUT, 256, 32, 4>(p, st);
+      return small ? launch<TIN, TOUT, 32, 32, 2>(p, st) : launch<TIN, TOUT, 64, 32, 4>(p, st);
     case 48: return big ? launch<TIN, TOUT, 256, 48, 4>(p, st) : launch<TIN, TOUT, 64, 48, 4>(p, st);
     case 64:
       if (big) return launch<TIN, TOUT, 256, 64, 4>(p, st);
-      return mid ? launch<TIN, TOUT, 128, 64, 4>(p, st) : launch<TIN, TOUT, 64, 64, 4>(p, st);
-    case 96: return big ? launch<TIN, TOUT, 128, 96, 2>(p, st) : launch<TIN, TOUT, 64, 96, 2>(p, st);
-    default: return big ? launch<TIN, TOUT, 128, 128, 2>(p, st) : launch<TIN, TOUT, 64, 128, 2>(p, st);
+      if (mid) return launch<TIN, TOUT, 128, 64, 4>(p, st);
+      return small ? launch<TIN, TOUT, 32, 64, 2>(p, st) : launch<TIN, TOUT, 64, 64, 4>(p, st);
+    case 96:
+      if (big) return launch<TIN, TOUT, 128, 96, 2>(p, st);
+      return small ? launch<TIN, TOUT, 32, 96, 2>(p, st) : launch<TIN, TOUT, 64, 96, 2>(p, st);
+    default:
+      if (big) return launch<TIN, TOUT, 128, 128, 2>(p, st);
+      return small ? launch<TIN, TOUT, 32, 128, 2>(p, st) : launch<TIN, TOUT, 64, 128, 2>(p, st);
   }
 }
 

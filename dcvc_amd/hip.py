@@ -109,8 +109,17 @@ def set_option(name, value):
     check(lib().dcvc_set_option(name.encode(), int(value)), "set_option")
 
 
+_raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+_get_device = getattr(torch._C, "_cuda_getDevice", None)
+
+
 def stream():
-    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    """Raw handle of torch's current HIP stream on the current device.  The
+    private torch._C accessors skip the Stream object torch.cuda.current_stream()
+    builds (~8 us per launch, measured on the P-frame loop)."""
+    if _raw_stream is not None and _get_device is not None:
+        return _raw_stream(_get_device())
+    return torch.cuda.current_stream().cuda_stream
 
 
 class Act:

@@ -336,6 +336,50 @@ def test_conv3x3_fixed_geometry_kernel(case):
         assert rel_err(outs[0][1], outs[1][1]) < 1e-5
 
 
+P3_CASES = [
+    # cin, cout, H, W, coff: grids of >= 2 tiles per CU so the persistent kernel takes them
+    (48, 48, 261, 533, 0), (96, 48, 130, 1030, 0), (64, 64, 270, 500, 8), (80, 48, 260, 520, 0),
+    (128, 64, 250, 530, 0), (96, 96, 200, 700, 0), (64, 128, 260, 520, 0), (32, 32, 300, 470, 16),
+]
+
+
+@pytest.mark.parametrize("case", P3_CASES)
+def test_conv3x3_persistent_kernel(case):
+    """The persistent resident-weight 3x3 kernel (conv3x3p.hip) is
+    bit-identical to the per-workgroup kernel (same K order, same fp32
+    epilogue order) with every epilogue option on: lrelu input, bias +
+    lrelu, two residuals, per-channel scale, ragged image edges, a channel
+    view of a wider input."""
+    h = K()
+    cin, cout, H, W, coff = case
+    x = torch.randn(1, cin + coff + 8, H, W)
+    w = torch.randn(cout, cin, 3, 3) / (9 * cin) ** 0.5
+    b = torch.randn(cout) * 0.1
+    cw = h.ConvW(w, b, 1, h.BF16)
+    xa = to_act(x, h.BF16).ch(coff, cin)
+    r1, r2 = to_act(torch.randn(1, cout, H, W), h.BF16), to_act(torch.randn(1, cout, H, W), h.BF16)
+    sc = (torch.rand(cout) + 0.5).cuda()
+    outs, names = [], []
+    for pers in (1, 0):
+        h.set_option("conv3x3_persistent", pers)
+        h.set_option("conv3x3_resident", 0)
+        y = h.conv(cw, xa, out_dtype=h.BF16, in_op=h.IN_LRELU, in_slope=0.1, act=h.ACT_LRELU, slope=0.01,
+                   res=r1, res2=r2, scale=sc)
+        names.append(h.lib().dcvc_last_kernel().decode())
+        y2 = h.conv(cw, xa, out_dtype=h.BF16)
+        torch.cuda.synchronize()
+        outs.append((back(y), back(y2)))
+    h.set_option("conv3x3_persistent", 1)
+    h.set_option("conv3x3_resident", 1)
+    assert names[0].startswith("conv3p_kernel"), names
+    assert not names[1].startswith("conv3p_kernel"), names
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert torch.equal(outs[0][1], outs[1][1])
+    xs = x[:, coff:coff + cin].bfloat16().float()
+    ref = F.conv2d(xs, w, b, padding=1)
+    assert rel_err(outs[0][1], ref) < 2e-2
+
+
 DCB_SHAPES = [(48, 32, False), (32, 64, False), (64, 128, False), (128, 128, False), (128, 64, False),
               (64, 48, False), (64, 64, False), (16, 32, True), (32, 64, True), (64, 128, True),
               (128, 128, True), (128, 64, True), (64, 16, True)]
