@@ -446,6 +446,8 @@ int dispatch(int cin, int cout, bool gated, bool adapt, const DcbP &p, hipStream
 
 }  // namespace
 
+extern "C" int dcvc_internal_dcbp(const dcvc_dcb_args *a, void *stream);
+
 extern "C" int dcvc_depthconv_block(const dcvc_dcb_args *a, void *stream) {
   if (!a || !a->x.ptr || !a->y.ptr) return DCVC_HIP_EINVAL;
   if (a->x.dtype != DCVC_BF16 || a->y.dtype != DCVC_BF16) return DCVC_HIP_EUNSUPPORTED;
@@ -455,6 +457,10 @@ extern "C" int dcvc_depthconv_block(const dcvc_dcb_args *a, void *stream) {
     return DCVC_HIP_EUNSUPPORTED;
   const bool adapt = a->w_adaptor != nullptr;
   if (!adapt && a->cin != a->cout) return DCVC_HIP_EINVAL;
+  {
+    const int r = dcvc_internal_dcbp(a, stream);  // persistent resident-weight kernel (dcbp.hip) first
+    if (r != DCVC_HIP_EUNSUPPORTED) return r;
+  }
   DcbP p{};
   p.x = reinterpret_cast<const uint16_t *>(a->x.ptr);
   p.H = a->x.H;

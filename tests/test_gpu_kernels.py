@@ -429,3 +429,27 @@ def test_fused_depthconv_block_matches_unfused(shape):
     fn = O.depth_conv_block2 if gated else O.depth_conv_block
     ref = fn(O.Params(sd), "b", x.to(torch.bfloat16).float()) * sc.view(1, -1, 1, 1)
     assert rel_err(outs[0], ref) < 3e-2
+
+
+@pytest.mark.parametrize("shape", [(64, 48), (48, 32), (32, 64), (64, 64)])
+def test_persistent_depthconv_block_equals_per_tile_kernel(shape):
+    """dcbp.hip (persistent, resident weights) vs dcb.hip on a map of >= 2
+    tiles per CU: same K order and rounding points, so bit-identical."""
+    from dcvc_amd import layers as L
+    h = K()
+    cin, cout = shape
+    sd = _dcb_state(cin, cout, False, seed=cin * 3 + cout)
+    ctx = L.Ctx(sd, torch.device("cuda"), L.Precision.fast())
+    blk = L.DepthConvBlock(ctx, "b")
+    H, W = 133, 541
+    xa = to_act(torch.randn(1, cin, H, W), h.BF16)
+    sc = (torch.rand(cout) + 0.5).cuda()
+    outs, names = [], []
+    for pers in (1, 0):
+        h.set_option("dcb_persistent", pers)
+        outs.append(back(blk(xa, scale=sc)))
+        names.append(h.lib().dcvc_last_kernel().decode())
+    h.set_option("dcb_persistent", 1)
+    torch.cuda.synchronize()
+    assert names[0].startswith("dcbp_kernel") and names[1].startswith("dcb_kernel"), names
+    assert torch.equal(outs[0], outs[1])
