@@ -39,11 +39,11 @@ struct P3 {
   int cinp;
   const float *bias;
   const float *scale;
-  uint16_t *y;
-  int ycs, yco;
-  const uint16_t *res;
+  void *y;
+  int ycs, yco, Wout;
+  const void *res;
   int rcs, rco;
-  const uint16_t *res2;
+  const void *res2;
   int r2cs, r2co;
   int cout;
   int in_lrelu;
@@ -55,6 +55,39 @@ struct P3 {
 };
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+// 8-element pieces of the output / residual type; an element index < 0
+// reads zeros (out-of-range buffer offset)
+template <typename T> struct Vec8;
+template <> struct Vec8<uint16_t> {
+  typedef u16x8 raw;
+  __device__ __forceinline__ static raw load(__amdgpu_buffer_rsrc_t r, int e) {
+    return __builtin_bit_cast(u16x8, __builtin_amdgcn_raw_buffer_load_b128(r, e < 0 ? 0x7ffffff0 : e * 2, 0, 0));
+  }
+  __device__ __forceinline__ static float get(const raw &v, int j) { return bf2f(v[j]); }
+  __device__ __forceinline__ static void store(uint16_t *p, const float v[8]) {
+    u16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = f2bf(v[j]);
+    *reinterpret_cast<u16x8 *>(p) = o;
+  }
+};
+typedef float f32x8 __attribute__((ext_vector_type(8)));
+template <> struct Vec8<float> {
+  typedef f32x8 raw;
+  __device__ __forceinline__ static raw load(__amdgpu_buffer_rsrc_t r, int e) {
+    const int o = e < 0 ? 0x7fffffe0 : e * 4;
+    const u32x4 a = __builtin_amdgcn_raw_buffer_load_b128(r, o, 0, 0);
+    const u32x4 b = __builtin_amdgcn_raw_buffer_load_b128(r, o + 16, 0, 0);
+    const f32x4 fa = __builtin_bit_cast(f32x4, a), fb = __builtin_bit_cast(f32x4, b);
+    return f32x8{fa[0], fa[1], fa[2], fa[3], fb[0], fb[1], fb[2], fb[3]};
+  }
+  __device__ __forceinline__ static float get(const raw &v, int j) { return v[j]; }
+  __device__ __forceinline__ static void store(float *p, const float v[8]) {
+    *reinterpret_cast<float4 *>(p) = make_float4(v[0], v[1], v[2], v[3]);
+    *reinterpret_cast<float4 *>(p + 4) = make_float4(v[4], v[5], v[6], v[7]);
+  }
+};
 
 __device__ __forceinline__ int swz(int row, int x, int slot) {
   return row * 32 + ((slot ^ (((x >> 2) & 1) << 1)) << 3);
@@ -82,10 +115,10 @@ struct Geo {
   static constexpr int PIX = IH * 18;
   static constexpr int PP = (PIX * QP + NTHR - 1) / NTHR; // input pieces per thread
   static constexpr int OQ = BN / 8;
-  static constexpr int PO = (TH * 16 * OQ + NTHR - 1) / NTHR;  // output pieces per thread
+  static constexpr int PO = (TH * 16 * OQ + NTHR - 1) / NTHR;  // output pieces per thread (either layout)
 };
 
-template <int CIN, int BN, int NW, int RW>
+template <int CIN, int BN, int NW, int RW, typename TOUT, bool SHUF>
 __global__ void __launch_bounds__(NW * 64) conv3p_kernel(P3 p) {
   typedef Geo<CIN, BN, NW, RW> G_;
   constexpr int NCH = G_::NCH, KS = G_::KS, NT = G_::NT, TH = G_::TH, IMG = G_::IMG;
@@ -185,8 +218,9 @@ __global__ void __launch_bounds__(NW * 64) conv3p_kernel(P3 p) {
   }
   for (int i = tid; i < BN; i += NTHR) {
     const int n = n0 + i;
+    const int cy = (SHUF ? n0 / 4 : n0) + i;  // scale is per output channel (after shuffle)
     Lc[i] = (p.bias && n < p.cout) ? p.bias[n] : 0.f;
-    Lc[BN + i] = (p.scale && n < p.cout) ? p.scale[n] : 1.f;
+    Lc[BN + i] = (p.scale && cy < (SHUF ? p.cout / 4 : p.cout)) ? p.scale[cy] : 1.f;
   }
 
   // per-lane MFMA operand bases (elements)
@@ -203,9 +237,9 @@ __global__ void __launch_bounds__(NW * 64) conv3p_kernel(P3 p) {
   }
   const uint16_t *LwA = Lw + swz(col, col, hi);
   const __amdgpu_buffer_rsrc_t rr =
-      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t *>(p.res), (short)0, p.rbytes, 0x00020000);
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p.res), (short)0, p.rbytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t rr2 =
-      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t *>(p.res2), (short)0, p.r2bytes, 0x00020000);
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p.res2), (short)0, p.r2bytes, 0x00020000);
 
   for (int t = g;;) {
     publish();
@@ -278,54 +312,68 @@ __global__ void __launch_bounds__(NW * 64) conv3p_kernel(P3 p) {
       }
     __syncthreads();
 
-    // ---- epilogue B: out = scale * (res2 + (res + v)), 16-byte bf16 pieces
+    // ---- epilogue B: out = scale * (res2 + (res + v)) in pieces of 8
+    // consecutive output channels of one output pixel, in output-row order
+    // (SHUF: conv channel n of pixel (y, x) is output channel n >> 2 of
+    // pixel (2y + (n >> 1 & 1), 2x + (n & 1)), pixel_shuffle(2))
     {
       const int oy0 = (t / p.tiles_x) * TH, ox0 = (t % p.tiles_x) * 16;
-      int64_t pix[PO];
-      int q8[PO];
+      constexpr int NQ = SHUF ? BN / 32 : BN / 8;  // pieces per (pixel, sub-position)
+      int64_t ob[PO];
+      int src[PO], cq[PO];
       bool ok[PO];
-      u16x8 r1[PO], r2[PO];
+      typename Vec8<TOUT>::raw r1[PO], r2[PO];
 #pragma unroll
       for (int u = 0; u < PO; ++u) {
         const int it = tid + u * NTHR;
-        const int l = it / OQ, q = it - (it / OQ) * OQ;
-        const int oy = oy0 + (l >> 4), ox = ox0 + (l & 15);
-        ok[u] = it < TH * 16 * OQ && oy < p.H && ox < p.W;
-        pix[u] = (int64_t)oy * p.W + ox;
-        q8[u] = q * 8;
-        if (p.res) {
-          const int off = ok[u] ? (int)(pix[u] * p.rcs + p.rco + n0 + q * 8) * 2 : 0x7ffffff0;
-          r1[u] = __builtin_bit_cast(u16x8, __builtin_amdgcn_raw_buffer_load_b128(rr, off, 0, 0));
+        const int q = it % NQ, r = it / NQ;
+        int l, oy, ox;
+        if constexpr (SHUF) {
+          const int dx = r & 1, cx = (r >> 1) & 15, dy = (r >> 5) & 1, cyl = r >> 6;
+          l = cyl * 16 + cx;
+          oy = 2 * (oy0 + cyl) + dy;
+          ox = 2 * (ox0 + cx) + dx;
+          ok[u] = it < TH * 16 * 4 * NQ && oy0 + cyl < p.H && ox0 + cx < p.W;
+          src[u] = l * LD + 4 * q * 8 + dy * 2 + dx;
+        } else {
+          l = r;
+          oy = oy0 + (l >> 4);
+          ox = ox0 + (l & 15);
+          ok[u] = it < TH * 16 * NQ && oy < p.H && ox < p.W;
+          src[u] = l * LD + q * 8;
         }
-        if (p.res2) {
-          const int off = ok[u] ? (int)(pix[u] * p.r2cs + p.r2co + n0 + q * 8) * 2 : 0x7ffffff0;
-          r2[u] = __builtin_bit_cast(u16x8, __builtin_amdgcn_raw_buffer_load_b128(rr2, off, 0, 0));
-        }
+        cq[u] = q * 8;
+        ob[u] = (int64_t)oy * p.Wout + ox;
+        const int cb = (SHUF ? n0 / 4 : n0) + q * 8;
+        if (p.res) r1[u] = Vec8<TOUT>::load(rr, ok[u] ? (int)(ob[u] * p.rcs + p.rco + cb) : -1);
+        if (p.res2) r2[u] = Vec8<TOUT>::load(rr2, ok[u] ? (int)(ob[u] * p.r2cs + p.r2co + cb) : -1);
       }
 #pragma unroll
       for (int u = 0; u < PO; ++u) {
         if (!ok[u]) continue;
-        const int it = tid + u * NTHR;
-        const int l = it / OQ;
-        const float4 a = *reinterpret_cast<const float4 *>(T + l * LD + q8[u]);
-        const float4 b = *reinterpret_cast<const float4 *>(T + l * LD + q8[u] + 4);
-        float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+        float v[8];
+        if constexpr (SHUF) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[j] = T[src[u] + 4 * j];
+        } else {
+          const float4 a = *reinterpret_cast<const float4 *>(T + src[u]);
+          const float4 b = *reinterpret_cast<const float4 *>(T + src[u] + 4);
+          v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+          v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+        }
         if (p.res) {
 #pragma unroll
-          for (int j = 0; j < 8; ++j) v[j] = bf2f(r1[u][j]) + v[j];
+          for (int j = 0; j < 8; ++j) v[j] = Vec8<TOUT>::get(r1[u], j) + v[j];
         }
         if (p.res2) {
 #pragma unroll
-          for (int j = 0; j < 8; ++j) v[j] = bf2f(r2[u][j]) + v[j];
+          for (int j = 0; j < 8; ++j) v[j] = Vec8<TOUT>::get(r2[u], j) + v[j];
         }
         if (p.scale) {
 #pragma unroll
-          for (int j = 0; j < 8; ++j) v[j] = v[j] * Lc[BN + q8[u] + j];
+          for (int j = 0; j < 8; ++j) v[j] = v[j] * Lc[BN + cq[u] + j];
         }
-        u16x8 o;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) o[j] = f2bf(v[j]);
-        *reinterpret_cast<u16x8 *>(p.y + pix[u] * p.ycs + p.yco + n0 + q8[u]) = o;
+        Vec8<TOUT>::store(reinterpret_cast<TOUT *>(p.y) + ob[u] * p.ycs + p.yco + (SHUF ? n0 / 4 : n0) + cq[u], v);
       }
     }
     if (!more) break;
@@ -337,7 +385,7 @@ __global__ void __launch_bounds__(NW * 64) conv3p_kernel(P3 p) {
 int g_cus = 0;
 int g_enabled = 1;
 
-template <int CIN, int BN, int NW, int RW>
+template <int CIN, int BN, int NW, int RW, typename TOUT, bool SHUF>
 int launch(P3 p, hipStream_t st) {
   typedef Geo<CIN, BN, NW, RW> G_;
   if constexpr (G_::LDS > 160 * 1024) {
@@ -354,12 +402,14 @@ int launch(P3 p, hipStream_t st) {
         return DCVC_HIP_ELAUNCH;
       g_cus = prop.multiProcessorCount;
     }
-    // a grid of fewer tiles than workgroups is better served per tile
-    if (ntiles < 2LL * g_cus) return DCVC_HIP_EUNSUPPORTED;
+    // a grid of fewer tiles than CUs is better served per tile
+    if (ntiles * p.nblk_n < g_cus) return DCVC_HIP_EUNSUPPORTED;
     int64_t G = g_cus / p.nblk_n;
-    if (G < 8) G = 8;
-    auto kern = conv3p_kernel<CIN, BN, NW, RW>;
-    dcvc_note_kernel("conv3p_kernel<%d, %d, %d, %d>@%lld", CIN, BN, NW, RW, (long long)G * p.nblk_n * NW * 64);
+    if (G > ntiles) G = ntiles;
+    if (G < 1) G = 1;
+    auto kern = conv3p_kernel<CIN, BN, NW, RW, TOUT, SHUF>;
+    dcvc_note_kernel("conv3p_kernel<%d, %d, %d, %d, %s, %s>@%lld", CIN, BN, NW, RW, tname<TOUT>(), bname(SHUF),
+                     (long long)G * p.nblk_n * NW * 64);
     (void)hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)G_::LDS);
     hipLaunchKernelGGL(kern, dim3((unsigned)(G * p.nblk_n)), dim3(NW * 64), G_::LDS, st, p);
@@ -369,17 +419,31 @@ int launch(P3 p, hipStream_t st) {
 }
 
 // 16 output rows per tile (8 waves x 2) when the LDS holds it, else 8.
-template <int CIN, int BN>
+template <int CIN, int BN, typename TOUT, bool SHUF>
 int pick_th(const P3 &p, hipStream_t st) {
-  if constexpr (Geo<CIN, BN, 8, 2>::LDS <= 160 * 1024) return launch<CIN, BN, 8, 2>(p, st);
-  return launch<CIN, BN, 8, 1>(p, st);
+  if constexpr (Geo<CIN, BN, 8, 2>::LDS <= 160 * 1024) return launch<CIN, BN, 8, 2, TOUT, SHUF>(p, st);
+  return launch<CIN, BN, 8, 1, TOUT, SHUF>(p, st);
 }
 
+// BN: 64 / 48 / 32 output channels per workgroup (a multiple of 32 with
+// shuffle, so every sub-position gets whole 8-channel pieces)
 template <int CIN>
-int pick_bn(const P3 &p, hipStream_t st) {
-  if (p.cout % 64 == 0 && Geo<CIN, 64, 8, 1>::LDS <= 160 * 1024) return pick_th<CIN, 64>(p, st);
-  if (p.cout % 48 == 0) return pick_th<CIN, 48>(p, st);
-  if (p.cout % 32 == 0) return pick_th<CIN, 32>(p, st);
+int pick_bn(const P3 &p, bool f32out, bool shuf, hipStream_t st) {
+  if (shuf) {
+    if (f32out) return DCVC_HIP_EUNSUPPORTED;
+    if (p.cout % 64 == 0 && Geo<CIN, 64, 8, 1>::LDS <= 160 * 1024) return pick_th<CIN, 64, uint16_t, true>(p, st);
+    if (p.cout % 32 == 0) return pick_th<CIN, 32, uint16_t, true>(p, st);
+    return DCVC_HIP_EUNSUPPORTED;
+  }
+  if (f32out) {
+    if (p.cout % 64 == 0 && Geo<CIN, 64, 8, 1>::LDS <= 160 * 1024) return pick_th<CIN, 64, float, false>(p, st);
+    if (p.cout % 48 == 0) return pick_th<CIN, 48, float, false>(p, st);
+    if (p.cout % 32 == 0) return pick_th<CIN, 32, float, false>(p, st);
+    return DCVC_HIP_EUNSUPPORTED;
+  }
+  if (p.cout % 64 == 0 && Geo<CIN, 64, 8, 1>::LDS <= 160 * 1024) return pick_th<CIN, 64, uint16_t, false>(p, st);
+  if (p.cout % 48 == 0) return pick_th<CIN, 48, uint16_t, false>(p, st);
+  if (p.cout % 32 == 0) return pick_th<CIN, 32, uint16_t, false>(p, st);
   return DCVC_HIP_EUNSUPPORTED;
 }
 
@@ -389,19 +453,19 @@ int pick_bn(const P3 &p, hipStream_t st) {
 // pixel shuffle; DCVC_HIP_EUNSUPPORTED hands the call on to conv3x3.hip.
 extern "C" int dcvc_internal_conv3p(const dcvc_conv_args *a, void *stream) {
   if (!g_enabled) return DCVC_HIP_EUNSUPPORTED;
-  if (a->x.dtype != DCVC_BF16 || a->y.dtype != DCVC_BF16 || a->shuffle) return DCVC_HIP_EUNSUPPORTED;
+  const bool f32out = a->y.dtype == DCVC_F32;
+  const int ye = f32out ? 4 : 2;
+  if (a->x.dtype != DCVC_BF16 || (a->y.dtype != DCVC_BF16 && !f32out)) return DCVC_HIP_EUNSUPPORTED;
   if (a->act != DCVC_ACT_NONE && a->act != DCVC_ACT_LRELU) return DCVC_HIP_EUNSUPPORTED;
   if (a->in_op != DCVC_IN_NONE && a->in_op != DCVC_IN_LRELU) return DCVC_HIP_EUNSUPPORTED;
   if (a->x.cstride % 8 || a->x.coff % 8 || ((uintptr_t)a->x.ptr & 15)) return DCVC_HIP_EUNSUPPORTED;
   if (a->y.cstride % 8 || a->y.coff % 8 || ((uintptr_t)a->y.ptr & 15) || a->cout % 8) return DCVC_HIP_EUNSUPPORTED;
-  if (a->res.ptr && (a->res.dtype != DCVC_BF16 || a->res.cstride % 8 || a->res.coff % 8 || ((uintptr_t)a->res.ptr & 15)))
-    return DCVC_HIP_EUNSUPPORTED;
-  if (a->res2.ptr &&
-      (a->res2.dtype != DCVC_BF16 || a->res2.cstride % 8 || a->res2.coff % 8 || ((uintptr_t)a->res2.ptr & 15)))
-    return DCVC_HIP_EUNSUPPORTED;
-  if ((int64_t)a->x.H * a->x.W * a->x.cstride >= ((int64_t)1 << 31) - 16) return DCVC_HIP_EUNSUPPORTED;
-  if ((int64_t)a->y.H * a->y.W * a->y.cstride >= ((int64_t)1 << 30) - 16) return DCVC_HIP_EUNSUPPORTED;
-  if ((int64_t)a->x.H * a->x.W * a->x.cstride >= ((int64_t)1 << 30) - 16) return DCVC_HIP_EUNSUPPORTED;
+  for (const dcvc_tensor *r : {&a->res, &a->res2})
+    if (r->ptr && (r->dtype != a->y.dtype || r->cstride % 8 || r->coff % 8 || ((uintptr_t)r->ptr & 15) ||
+                   (int64_t)r->H * r->W * r->cstride * ye >= ((int64_t)1 << 31) - 64))
+      return DCVC_HIP_EUNSUPPORTED;
+  if ((int64_t)a->x.H * a->x.W * a->x.cstride * 2 >= ((int64_t)1 << 31) - 64) return DCVC_HIP_EUNSUPPORTED;
+  if ((int64_t)a->y.H * a->y.W * a->y.cstride * ye >= ((int64_t)1 << 31) - 64) return DCVC_HIP_EUNSUPPORTED;
   P3 p{};
   p.x = reinterpret_cast<const uint16_t *>(a->x.ptr);
   p.H = a->x.H;
@@ -412,35 +476,37 @@ extern "C" int dcvc_internal_conv3p(const dcvc_conv_args *a, void *stream) {
   p.cinp = (a->cin + 31) / 32 * 32;
   p.bias = a->bias;
   p.scale = a->scale;
-  p.y = reinterpret_cast<uint16_t *>(a->y.ptr);
+  p.y = a->y.ptr;
   p.ycs = a->y.cstride;
   p.yco = a->y.coff;
+  p.Wout = a->y.W;
   if (a->res.ptr) {
-    p.res = reinterpret_cast<const uint16_t *>(a->res.ptr);
+    p.res = a->res.ptr;
     p.rcs = a->res.cstride;
     p.rco = a->res.coff;
+    p.rbytes = a->res.H * a->res.W * a->res.cstride * ye;
   }
   if (a->res2.ptr) {
-    p.res2 = reinterpret_cast<const uint16_t *>(a->res2.ptr);
+    p.res2 = a->res2.ptr;
     p.r2cs = a->res2.cstride;
     p.r2co = a->res2.coff;
+    p.r2bytes = a->res2.H * a->res2.W * a->res2.cstride * ye;
   }
   p.xbytes = a->x.H * a->x.W * a->x.cstride * 2;
-  if (a->res.ptr) p.rbytes = a->res.H * a->res.W * a->res.cstride * 2;
-  if (a->res2.ptr) p.r2bytes = a->res2.H * a->res2.W * a->res2.cstride * 2;
   p.cout = a->cout;
   p.in_lrelu = a->in_op == DCVC_IN_LRELU;
   p.in_slope = a->in_slope;
   p.act = a->act;
   p.slope = a->slope;
+  const bool shuf = a->shuffle != 0;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   switch (a->cin) {
-    case 32: return pick_bn<32>(p, st);
-    case 48: return pick_bn<48>(p, st);
-    case 64: return pick_bn<64>(p, st);
-    case 80: return pick_bn<80>(p, st);
-    case 96: return pick_bn<96>(p, st);
-    case 128: return pick_bn<128>(p, st);
+    case 32: return pick_bn<32>(p, f32out, shuf, st);
+    case 48: return pick_bn<48>(p, f32out, shuf, st);
+    case 64: return pick_bn<64>(p, f32out, shuf, st);
+    case 80: return pick_bn<80>(p, f32out, shuf, st);
+    case 96: return pick_bn<96>(p, f32out, shuf, st);
+    case 128: return pick_bn<128>(p, f32out, shuf, st);
     default: return DCVC_HIP_EUNSUPPORTED;
   }
 }

@@ -359,6 +359,10 @@ def test_conv3x3_persistent_kernel(case):
     xa = to_act(x, h.BF16).ch(coff, cin)
     r1, r2 = to_act(torch.randn(1, cout, H, W), h.BF16), to_act(torch.randn(1, cout, H, W), h.BF16)
     sc = (torch.rand(cout) + 0.5).cuda()
+    rf = to_act(torch.randn(1, cout, H, W), h.F32)
+    shuf = cout % 32 == 0
+    r3 = to_act(torch.randn(1, cout // 4, 2 * H, 2 * W), h.BF16) if shuf else None
+    sc4 = (torch.rand(cout // 4) + 0.5).cuda() if shuf else None
     outs, names = [], []
     for pers in (1, 0):
         h.set_option("conv3x3_persistent", pers)
@@ -367,17 +371,28 @@ def test_conv3x3_persistent_kernel(case):
                    res=r1, res2=r2, scale=sc)
         names.append(h.lib().dcvc_last_kernel().decode())
         y2 = h.conv(cw, xa, out_dtype=h.BF16)
+        y3 = h.conv(cw, xa, out_dtype=h.F32, act=h.ACT_LRELU, slope=0.1, res=rf)
+        names.append(h.lib().dcvc_last_kernel().decode())
+        got = [back(y), back(y2), back(y3)]
+        if shuf:
+            y4 = h.conv(cw, xa, out_dtype=h.BF16, shuffle=True, res=r3, scale=sc4)
+            names.append(h.lib().dcvc_last_kernel().decode())
+            got.append(back(y4))
         torch.cuda.synchronize()
-        outs.append((back(y), back(y2)))
+        outs.append(got)
     h.set_option("conv3x3_persistent", 1)
     h.set_option("conv3x3_resident", 1)
-    assert names[0].startswith("conv3p_kernel"), names
-    assert not names[1].startswith("conv3p_kernel"), names
-    assert torch.equal(outs[0][0], outs[1][0])
-    assert torch.equal(outs[0][1], outs[1][1])
+    k = len(names) // 2
+    assert all(n.startswith("conv3p_kernel") for n in names[:k]), names
+    assert not any(n.startswith("conv3p_kernel") for n in names[k:]), names
+    for a, b_ in zip(outs[0], outs[1]):
+        assert torch.equal(a, b_)
     xs = x[:, coff:coff + cin].bfloat16().float()
     ref = F.conv2d(xs, w, b, padding=1)
     assert rel_err(outs[0][1], ref) < 2e-2
+    if shuf:
+        ref4 = F.pixel_shuffle(ref, 2) * sc4.cpu().view(1, -1, 1, 1)
+        assert rel_err(outs[0][3] - back(r3) * sc4.cpu().view(1, -1, 1, 1), ref4) < 2e-2
 
 
 DCB_SHAPES = [(48, 32, False), (32, 64, False), (64, 128, False), (128, 128, False), (128, 64, False),
