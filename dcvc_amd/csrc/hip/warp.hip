@@ -77,6 +77,32 @@ __global__ void warp_kernel(View x, View f, View y, const float *gx, const float
     st<TY>(y.p, pix * y.cs + y.co + c, sample<TX>(x, b, c));
 }
 
+// Vector form for bf16 maps with 8-channel-aligned views: one thread per
+// (pixel, 8 channels), 16-byte corner loads and one 16-byte store instead of
+// 32 two-byte loads (the scalar kernel is load-instruction bound).  Same
+// per-channel arithmetic, so results are identical.
+__global__ void warp8_kernel(View x, View f, View y, const float *gx, const float *gy) {
+  const int q8 = y.C >> 3;
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t pix = t / q8;
+  if (pix >= (int64_t)y.H * y.W) return;
+  const int c = (int)(t - pix * q8) * 8;
+  const int py = (int)(pix / y.W), px = (int)(pix - (int64_t)py * y.W);
+  const float2 fv = *reinterpret_cast<const float2 *>(reinterpret_cast<const float *>(f.p) + pix * f.cs + f.co);
+  const Bilin b = warp_coords(gx[px], gy[py], fv.x, fv.y, x.W, x.H);
+  const uint16_t *xp = reinterpret_cast<const uint16_t *>(x.p) + x.co + c;
+  const int64_t r0 = (int64_t)b.y0 * x.W, r1 = (int64_t)b.y1 * x.W;
+  const u16x8 a = *reinterpret_cast<const u16x8 *>(xp + (r0 + b.x0) * x.cs);
+  const u16x8 bb = *reinterpret_cast<const u16x8 *>(xp + (r0 + b.x1) * x.cs);
+  const u16x8 cc = *reinterpret_cast<const u16x8 *>(xp + (r1 + b.x0) * x.cs);
+  const u16x8 d = *reinterpret_cast<const u16x8 *>(xp + (r1 + b.x1) * x.cs);
+  u16x8 o;
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+    o[j] = f2bf(bf2f(a[j]) * b.nw + bf2f(bb[j]) * b.ne + bf2f(cc[j]) * b.sw + bf2f(d[j]) * b.se);
+  *reinterpret_cast<u16x8 *>(reinterpret_cast<uint16_t *>(y.p) + pix * y.cs + y.co + c) = o;
+}
+
 // bilinear x2 upsample value of channel c at full-res pixel (oy, ox) from a
 // half-res map (align_corners=False, UpSampleKernel.cpp cpu_upsample_linear)
 template <typename T>
@@ -110,16 +136,49 @@ __global__ void offset_div_kernel(View feat, View offs, View flow, View y, const
   const int py = (int)(pix / y.W), px = (int)(pix - (int64_t)py * y.W);
   const float fx = ld<float>(flow.p, pix * flow.cs + flow.co);
   const float fy = ld<float>(flow.p, pix * flow.cs + flow.co + 1);
+  // bilinear x2 upsample of the half-resolution offset map (up2_at), the
+  // corner geometry shared by this group's 4 offset and 2 mask channels
+  float sy = 0.5f * ((float)py + 0.5f) - 0.5f;
+  float sx = 0.5f * ((float)px + 0.5f) - 0.5f;
+  sy = sy < 0.f ? 0.f : sy;
+  sx = sx < 0.f ? 0.f : sx;
+  const int h0 = (int)sy, w0 = (int)sx;
+  const int h1 = h0 + (h0 < offs.H - 1 ? 1 : 0), w1 = w0 + (w0 < offs.W - 1 ? 1 : 0);
+  const float hl1 = sy - (float)h0, hl0 = 1.f - hl1;
+  const float wl1 = sx - (float)w0, wl0 = 1.f - wl1;
+  float ov[6];  // offset channels 4g..4g+3 (dx, dy of warps 2g, 2g+1), mask channels 64+2g, 65+2g
+  {
+    const int64_t e[4] = {((int64_t)h0 * offs.W + w0) * offs.cs + offs.co, ((int64_t)h0 * offs.W + w1) * offs.cs + offs.co,
+                          ((int64_t)h1 * offs.W + w0) * offs.cs + offs.co, ((int64_t)h1 * offs.W + w1) * offs.cs + offs.co};
+    float cv[4][6];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      if constexpr (sizeof(TO) == 4) {
+        const float *op = reinterpret_cast<const float *>(offs.p) + e[k];
+        const float4 o4 = *reinterpret_cast<const float4 *>(op + 4 * g);
+        const float2 m2 = *reinterpret_cast<const float2 *>(op + 64 + 2 * g);
+        cv[k][0] = o4.x; cv[k][1] = o4.y; cv[k][2] = o4.z; cv[k][3] = o4.w;
+        cv[k][4] = m2.x; cv[k][5] = m2.y;
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) cv[k][j] = ld<TO>(offs.p, e[k] + 4 * g + j);
+        cv[k][4] = ld<TO>(offs.p, e[k] + 64 + 2 * g);
+        cv[k][5] = ld<TO>(offs.p, e[k] + 65 + 2 * g);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 6; ++j) ov[j] = (cv[0][j] * wl0 + cv[1][j] * wl1) * hl0 + (cv[2][j] * wl0 + cv[3][j] * wl1) * hl1;
+  }
   float xm[6];
 #pragma unroll
   for (int k = 0; k < 2; ++k) {
     const int i = 2 * g + k;                       // warp index 0..31
     // offset channels 2i, 2i+1 of cat(o1, o2) = channels 2i, 2i+1 of the map
-    float dx = mag * tanhf(up2_at<TO>(offs, py, px, 2 * i));
-    float dy = mag * tanhf(up2_at<TO>(offs, py, px, 2 * i + 1));
+    float dx = mag * tanhf(ov[2 * k]);
+    float dy = mag * tanhf(ov[2 * k + 1]);
     dx = dx + fx;                                  // flow.repeat: even ch -> dx
     dy = dy + fy;
-    const float msk = sigmoidf_(up2_at<TO>(offs, py, px, 64 + i));
+    const float msk = sigmoidf_(ov[4 + k]);
     const Bilin b = warp_coords(gx[px], gy[py], dx, dy, feat.W, feat.H);
     const int src_group = i & 15;                  // x.repeat(2,1,1,1)
 #pragma unroll
@@ -212,6 +271,15 @@ extern "C" int dcvc_flow_warp(dcvc_tensor x, dcvc_tensor flow, dcvc_tensor y, co
       x.W != y.W || x.C != y.C)
     return DCVC_HIP_EINVAL;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (x.dtype == DCVC_BF16 && y.dtype == DCVC_BF16 && y.C % 8 == 0 && x.cstride % 8 == 0 && x.coff % 8 == 0 &&
+      y.cstride % 8 == 0 && y.coff % 8 == 0 && flow.cstride % 2 == 0 && flow.coff % 2 == 0 &&
+      ((uintptr_t)x.ptr & 15) == 0 && ((uintptr_t)y.ptr & 15) == 0 && ((uintptr_t)flow.ptr & 7) == 0) {
+    const int64_t total = (int64_t)y.H * y.W * (y.C / 8);
+    hipLaunchKernelGGL(warp8_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, mk(x), mk(flow),
+                       mk(y), gx, gy);
+    DCVC_LAUNCH_CHECK();
+    return DCVC_HIP_OK;
+  }
   const int tpc = y.C >= 32 ? 32 : (y.C >= 8 ? 8 : 4);  // threads per pixel
   const int ppb = 256 / tpc;
   const int64_t npix = (int64_t)y.H * y.W;
@@ -234,6 +302,8 @@ extern "C" int dcvc_offset_diversity(dcvc_tensor feat, dcvc_tensor offs, dcvc_te
       feat.H != y.H || feat.W != y.W || flow.H != y.H || flow.W != y.W ||
       offs.H * 2 != y.H || offs.W * 2 != y.W)
     return DCVC_HIP_EINVAL;
+  if (offs.dtype == DCVC_F32 && (offs.cstride % 4 || offs.coff % 4 || ((uintptr_t)offs.ptr & 15)))
+    return DCVC_HIP_EUNSUPPORTED;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const int64_t threads = (int64_t)y.H * y.W * 16;
   const unsigned grd = (unsigned)((threads + 255) / 256);

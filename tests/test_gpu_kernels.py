@@ -174,6 +174,25 @@ def test_flow_warp_matches_reference_formula():
     assert (back(y) - ref).abs().max().item() < 1e-5
 
 
+def test_flow_warp_bf16_vector_path():
+    """bf16 maps with 8-channel-aligned views take the 16-byte-per-corner
+    kernel: per-channel arithmetic in fp32 from the bf16 inputs, one bf16
+    rounding, i.e. the reference formula on the bf16-rounded input."""
+    from oracle.dc_oracle import flow_warp
+    h = K()
+    H, W = 33, 47
+    x = torch.randn(1, 64, H, W)
+    flow = torch.randn(1, 2, H, W) * 6
+    xa = to_act(x, h.BF16)
+    y = h.empty(H, W, 56, h.BF16)
+    h.flow_warp(xa.ch(8, 48), to_act(flow, h.F32), _grid(H, W), y=y.ch(8, 48))
+    torch.cuda.synchronize()
+    ref = flow_warp(x[:, 8:56].bfloat16().float(), flow).bfloat16().float()
+    got = back(y)[:, 8:56]
+    assert (got - ref).abs().max().item() <= 1e-2 * ref.abs().max().item()
+    assert (got == ref).float().mean().item() > 0.99
+
+
 def test_resize_and_pool():
     from oracle.dc_oracle import up2, down2
     h = K()
