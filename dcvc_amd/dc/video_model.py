@@ -61,7 +61,7 @@ class DMC:
         self.grids = Grids(self.dev)
         self.optic_flow = SpyNet(ctx, "optic_flow", self.grids)
         # OffsetDiversity (video_model.py:26-63)
-        self.off_c0 = ctx.conv("align.conv_offset.0", 2)
+        self.off_c0 = ctx.conv("align.conv_offset.0", 2, cin_pad=56)
         self.off_c2 = ctx.conv("align.conv_offset.2")
         self.off_c4 = ctx.conv("align.conv_offset.4")
         self.fusion_w = ctx.take("align.fusion.weight").detach().float().reshape(48, 6).contiguous().to(self.dev)
@@ -104,7 +104,7 @@ class DMC:
         self.cf_c1out, self.cf_r1out = ctx.conv(cf + ".conv1_out"), ResBlock(ctx, cf + ".res_block1_out")
         # contextual encoder / decoder / recon (video_model.py:173-232)
         ce = "contextual_encoder"
-        self.ce_c1 = ctx.conv(ce + ".conv1", 2)
+        self.ce_c1 = ctx.conv(ce + ".conv1", 2, cin_pad=56)
         self.ce_r1 = ResBlock(ctx, ce + ".res1", 0.1, True)
         self.ce_c2 = ctx.conv(ce + ".conv2", 2)
         self.ce_r2 = ResBlock(ctx, ce + ".res2", 0.1, True)
@@ -133,6 +133,7 @@ class DMC:
         self.fine = {k: q_fine(sd[k]) for k in
                      ("mv_y_q_scale_enc", "mv_y_q_scale_dec", "y_q_scale_enc", "y_q_scale_dec")}
         self._q_cache = {}
+        self._zpad = {}
         if strict:
             ctx.check_strict([k for k in sd if k.startswith("bit_estimator") or "_q_" in k])
         return self
@@ -172,6 +173,14 @@ class DMC:
                 out.append(curr_q(table, self.sd[basic], q_index, self.dev))
             self._q_cache[key] = out
         return self._q_cache[key]
+
+    def _padded(self, key, H, W, C):
+        """A cached concat buffer of C channels whose channels beyond the ones
+        the producers write stay zero (allocated zeroed once per shape)."""
+        k = (key, H, W)
+        if k not in self._zpad:
+            self._zpad[k] = K.zeros(H, W, C, self.prec.feat, self.dev)
+        return self._zpad[k]
 
     # ---------------------------------------------------------- sub-graphs
     def _mv_encoder(self, est_mv, ref_mv_feature, q):
@@ -234,7 +243,7 @@ class DMC:
         feat, dev = self.prec.feat, self.dev
         H, W = mv.H, mv.W
         ref = dpb["ref_frame"]
-        aux = K.empty(H, W, G1 + 3 + 2, feat, dev)                    # cat(c1_init, warpframe, mv)
+        aux = self._padded("aux", H, W, 56)                             # cat(c1_init, warpframe, mv, 0 x3)
         K.flow_warp(ref, mv, self.grids(H, W), y=aux.ch(G1, 3))
         mv2 = K.resize2x(mv, False, 0.5)
         mv3 = K.resize2x(mv2, False, 0.5)
@@ -247,7 +256,7 @@ class DMC:
         r3 = self.fe_r3(K.conv(self.fe_c3, r2))
         K.flow_warp(r1, mv, self.grids(H, W), y=aux.ch(0, G1))
         K.copy(mv, aux.ch(G1 + 3, 2))
-        o = K.conv(self.off_c0, aux, act=ACT_LRELU, slope=0.1)
+        o = K.conv(self.off_c0, aux, act=ACT_LRELU, slope=0.1)  # 56 = 53 + 3 zero channels
         o = K.conv(self.off_c2, o, act=ACT_LRELU, slope=0.1)
         o = K.conv(self.off_c4, o, out_dtype=F32)
         cat1 = K.empty(H, W, G1 + G1, feat, dev)                       # cat(c2_up, c1)
@@ -265,7 +274,7 @@ class DMC:
 
     def _contextual_encoder(self, x, c1, c2, c3, q):
         feat, dev = self.prec.feat, self.dev
-        cat = K.empty(x.H, x.W, 3 + G1, feat, dev)
+        cat = self._padded("ce", x.H, x.W, 56)                         # cat(x, c1, 0 x5)
         K.copy(x, cat.ch(0, 3))
         K.copy(c1, cat.ch(3, G1))
         cat2 = K.empty(c2.H, c2.W, G2 + G2, feat, dev)

@@ -62,11 +62,18 @@ class Ctx:
         if unused:
             raise RuntimeError(f"unexpected key(s) in state_dict: {sorted(unused)[:8]}")
 
-    def conv(self, name, stride=1, latent=False, compute=None):
+    def conv(self, name, stride=1, latent=False, compute=None, cin_pad=None):
+        """cin_pad: zero-pad the input channels to this count, for inputs whose
+        concat buffer carries zero channels up to an 8-channel multiple (the
+        kernels' 16-byte staging path); the products of the pad are exact
+        zeros, so the result is unchanged."""
         if compute is None:
             compute = self.prec.latent_compute if latent else self.prec.feat_compute
         b = self.take(name + ".bias") if name + ".bias" in self.sd else None
-        return K.ConvW(self.take(name + ".weight"), b, stride, compute, self.dev)
+        w = self.take(name + ".weight")
+        if cin_pad is not None and cin_pad > w.shape[1]:
+            w = torch.nn.functional.pad(w.detach().float(), (0, 0, 0, 0, 0, cin_pad - w.shape[1]))
+        return K.ConvW(w, b, stride, compute, self.dev)
 
     def dw(self, name):
         w = self.take(name + ".weight").detach().float().cpu()  # [C,1,3,3]
