@@ -205,6 +205,80 @@ __global__ void qt_encode_kernel(QT t, int k, int16_t *sym, int16_t *idx, float 
   st<float>(t.yhat.p, pix * t.yhat.cs + t.yhat.co + ch, yh * qs);
 }
 
+// ---- estimate mode (forward_four_part_prior + get_y_*_bits,
+// common_model.py:39-58): y_q and its step's scale give the element's bits;
+// the same quantise / y_hat outputs as qt_encode_kernel.
+__device__ __forceinline__ float probs_to_bits(float p) {
+  // -1.0 * log(p + 1e-5) / log(2.0), clamp_min 0 (common_model.py:39-43)
+  const float b = -1.f * logf(p + 1e-5f) / 0.6931471805599453f;
+  return b > 0.f ? b : 0.f;
+}
+__device__ __forceinline__ float dist_cdf(int gaussian, float v, float s) {
+  if (gaussian) return 0.5f * (1.f + erff(v * (1.f / s) / 1.4142135623730951f));  // Normal(0, s).cdf
+  const float sg = v > 0.f ? 1.f : (v < 0.f ? -1.f : 0.f);
+  return 0.5f - 0.5f * sg * expm1f(-fabsf(v) / s);                                  // Laplace(0, s).cdf
+}
+
+__global__ void qt_estimate_kernel(QT t, int k, float *bits, int gaussian) {
+  const int C4 = t.C / 4;
+  const int64_t HW = (int64_t)t.y.H * t.y.W;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= HW * C4) return;
+  const int cc = (int)(i / HW);
+  const int64_t pix = i - (int64_t)cc * HW;
+  const int py = (int)(pix / t.y.W), px = (int)(pix - (int64_t)py * t.y.W);
+  const int q = quarter_of(k, ((py & 1) << 1) | (px & 1));
+  const int ch = q * C4 + cc;
+  float qs = ld<float>(t.params.p, pix * t.params.cs + t.params.co + ch);
+  qs = fmaxf(qs, 0.5f);
+  const float yv = ld<float>(t.y.p, pix * t.y.cs + t.y.co + ch) / qs;
+  float sc, me;
+  step_scales_means(t, pix, q, cc, sc, me);
+  const float yq = rintf(yv - me);
+  const float yh = yq + me;
+  const float s = fminf(fmaxf(sc, 1e-5f), 1e10f);       // sigma.clamp(1e-5, 1e10)
+  bits[i] = probs_to_bits(dist_cdf(gaussian, yq + 0.5f, s) - dist_cdf(gaussian, yq - 0.5f, s));
+  st<float>(t.yhs.p, pix * t.yhs.cs + t.yhs.co + ch, yh);
+  st<float>(t.yhat.p, pix * t.yhat.cs + t.yhat.co + ch, yh * qs);
+}
+
+// BitEstimator.get_cdf (entropy_models.py:56-122) at z +- 0.5 -> bits;
+// tab[c][11] = softplus(h1), b1, tanh(a1), ..., softplus(h4), b4
+__device__ __forceinline__ float factorized_cdf(const float *t, float x) {
+#pragma unroll
+  for (int l = 0; l < 3; ++l) {
+    x = x * t[3 * l] + t[3 * l + 1];
+    x = x + tanhf(x) * t[3 * l + 2];
+  }
+  x = x * t[9] + t[10];
+  return 1.f / (1.f + expf(-x));
+}
+
+__global__ void factorized_bits_kernel(View z, const float *tab, float *bits) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)z.H * z.W * z.C) return;
+  const int c = (int)(i % z.C);
+  const int64_t pix = i / z.C;
+  const float v = ld<float>(z.p, pix * z.cs + z.co + c);
+  const float *t = tab + c * 11;
+  bits[i] = probs_to_bits(factorized_cdf(t, v + 0.5f) - factorized_cdf(t, v - 0.5f));
+}
+
+// deterministic sum of n floats: one 1024-thread block, fixed strides and
+// a fixed tree, so the total is reproducible run to run
+__global__ void __launch_bounds__(1024) sum_kernel(const float *x, int64_t n, float *out) {
+  __shared__ float part[1024];
+  float a = 0.f;
+  for (int64_t i = threadIdx.x; i < n; i += 1024) a += x[i];
+  part[threadIdx.x] = a;
+  __syncthreads();
+  for (int w = 512; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) part[threadIdx.x] += part[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *out = part[0];
+}
+
 __global__ void qt_index_kernel(QT t, int k, int16_t *idx, float log_min, float log_step) {
   const int C4 = t.C / 4;
   const int64_t HW = (int64_t)t.params.H * t.params.W;
@@ -413,6 +487,42 @@ extern "C" int dcvc_symbols_to_nhwc(const int16_t *symbols, dcvc_tensor y, void 
     hipLaunchKernelGGL((from_sym_kernel<float>), dim3(g), dim3(256), 0, st, symbols, mk(y));
   else
     hipLaunchKernelGGL((from_sym_kernel<uint16_t>), dim3(g), dim3(256), 0, st, symbols, mk(y));
+  DCVC_LAUNCH_CHECK();
+  return DCVC_HIP_OK;
+}
+
+extern "C" int dcvc_quadtree_estimate_step(dcvc_tensor y, dcvc_tensor params, dcvc_tensor sm, int k,
+                                           dcvc_tensor yhs, dcvc_tensor yhat, float *bits, int gaussian,
+                                           void *stream) {
+  const int C = y.C;
+  if (!ok(y) || y.dtype != DCVC_F32 || !qt_ok(params, sm, C) || k < 0 || k > 3) return DCVC_HIP_EINVAL;
+  if ((k == 0) != (sm.ptr == nullptr)) return DCVC_HIP_EINVAL;
+  if (!ok(yhs) || !ok(yhat) || yhs.dtype != DCVC_F32 || yhat.dtype != DCVC_F32 || yhs.C != C ||
+      yhat.C != C || !bits)
+    return DCVC_HIP_EINVAL;
+  if (params.H != y.H || params.W != y.W || yhs.H != y.H || yhat.H != y.H || yhs.W != y.W || yhat.W != y.W)
+    return DCVC_HIP_EINVAL;
+  QT t{mk(y), mk(params), mk(sm), mk(yhs), mk(yhat), sm.ptr != nullptr, C};
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const unsigned g = blocks_for((int64_t)y.H * y.W * (C / 4));
+  hipLaunchKernelGGL(qt_estimate_kernel, dim3(g), dim3(256), 0, st, t, k, bits, gaussian ? 1 : 0);
+  DCVC_LAUNCH_CHECK();
+  return DCVC_HIP_OK;
+}
+
+extern "C" int dcvc_factorized_bits(dcvc_tensor z, const float *table, float *bits, void *stream) {
+  if (!ok(z) || z.dtype != DCVC_F32 || !table || !bits) return DCVC_HIP_EINVAL;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(factorized_bits_kernel, dim3(blocks_for((int64_t)z.H * z.W * z.C)), dim3(256), 0, st, mk(z),
+                     table, bits);
+  DCVC_LAUNCH_CHECK();
+  return DCVC_HIP_OK;
+}
+
+extern "C" int dcvc_sum_f32(const float *x, int64_t n, float *out, void *stream) {
+  if (!x || !out || n < 0) return DCVC_HIP_EINVAL;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(sum_kernel, dim3(1), dim3(1024), 0, st, x, n, out);
   DCVC_LAUNCH_CHECK();
   return DCVC_HIP_OK;
 }

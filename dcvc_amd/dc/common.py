@@ -83,6 +83,18 @@ class QuadtreePrior:
                              symbuf.idx_slice(calls[k]), scale_table.log_min, scale_table.log_step)
         return yhat
 
+    def estimate(self, y, buf, bits, gaussian):
+        """forward_four_part_prior (write=False) on the GPU: y_hat and, per
+        element, its estimated bits (bits: fp32 device tensor of C*h*w)."""
+        C = self.C
+        yhat = K.empty(y.H, y.W, C, F32, self.ctx.dev)
+        params = buf.ch(C, 3 * C)
+        n = y.H * y.W * (C // 4)
+        for k in range(4):
+            sm = None if k == 0 else self.step_params(buf, k)
+            K.qt_estimate_step(y, params, sm, k, buf.ch(0, C), yhat, bits[k * n:(k + 1) * n], gaussian)
+        return yhat
+
     def decode(self, buf, decode_fn, scale_table):
         """decode_fn(host int16 indexes) -> host int16 symbols."""
         C = self.C
@@ -104,6 +116,48 @@ class QuadtreePrior:
             sym_d.copy_(sym_h, non_blocking=True)
             K.qt_decode_step(params, sm, k, sym_d, buf.ch(0, C), yhat)
         return yhat
+
+
+class BitCounter:
+    """Estimate-mode bit totals on the GPU: per-element bits buffers summed
+    in a fixed order (dcvc_sum_f32), one host transfer for all totals."""
+
+    def __init__(self, device, names):
+        self.dev = device
+        self.names = list(names)
+        self.tot = torch.empty(len(self.names), dtype=torch.float32, device=device)
+        self.bufs = {}
+
+    def buffer(self, name, n):
+        b = torch.empty(n, dtype=torch.float32, device=self.dev)
+        self.bufs[name] = b
+        return b
+
+    def factorized(self, name, z, table):
+        b = self.buffer(name, z.H * z.W * z.C)
+        K.factorized_bits(z, table.chain_on(self.dev), b)
+
+    def totals(self):
+        for i, n in enumerate(self.names):
+            K.sum_f32(self.bufs[n], self.tot[i:i + 1])
+        host = self.tot.cpu().numpy()
+        return {n: np.float32(host[i]) for i, n in enumerate(self.names)}
+
+
+def bits_result(tot, pixel_num, names):
+    """bpp_k = sum(bits_k) / pixel_num, bit = sum(bpp) * pixel_num, in fp32
+    as the reference computes them (video_model.py:602-612)."""
+    n = np.float32(pixel_num)
+    bpp = {k: np.float32(tot[k]) / n for k in names}
+    total = np.float32(0)
+    for k in names:
+        total = np.float32(total + bpp[k])
+    out = {"bpp_" + k: float(bpp[k]) for k in names}
+    out["bpp"] = float(total)
+    out["bit"] = float(np.float32(total * n))
+    for k in names:
+        out["bit_" + k] = float(np.float32(bpp[k] * n))
+    return out
 
 
 def pad_for_y(y):
@@ -137,4 +191,4 @@ def curr_q(table, basic, q_index, device):
     return q.reshape(-1).contiguous().to(device)
 
 
-__all__ = ["SymbolBuffer", "QuadtreePrior", "pad_for_y", "crop_to", "q_fine", "curr_q", "cast"]
+__all__ = ["SymbolBuffer", "QuadtreePrior", "BitCounter", "bits_result", "pad_for_y", "crop_to", "q_fine", "curr_q", "cast"]

@@ -2,8 +2,8 @@
 
 API of DCVC-DC/src/models/image_model.py:61-252: ``IntraNoAR(N, anchor_num,
 ec_thread, stream_part, inplace)``, ``load_state_dict``, ``update``,
-``get_q_scales_from_ckpt``, ``compress``, ``decompress``, ``encode_decode``
-(write mode).  ``x_hat`` is an NHWC fp32 ``Act``.
+``get_q_scales_from_ckpt``, ``compress``, ``decompress``, ``forward``
+(estimate mode) and ``encode_decode`` (both modes).  ``x_hat`` is an NHWC fp32 ``Act``.
 """
 import torch
 
@@ -12,7 +12,7 @@ from ..hip import F32, ACT_LRELU, ACT_CLAMP01
 from ..layers import Ctx, Precision, DepthConvBlock, ResidualBlockWithStride, ResidualBlockUpsample, UNet
 from ..entropy import ScaleTable, FactorizedTable, EntropyCoder
 from ..stream_helper import get_downsampled_shape, encode_i, decode_i, filesize, get_state_dict
-from .common import SymbolBuffer, QuadtreePrior, pad_for_y, crop_to, q_fine, curr_q
+from .common import SymbolBuffer, QuadtreePrior, BitCounter, bits_result, pad_for_y, crop_to, q_fine, curr_q
 from .video_model import as_act
 
 
@@ -102,28 +102,49 @@ class IntraNoAR:
         crop_to(full, yh, yw, y=buf.ch(self.N, 3 * self.N))
         return buf
 
-    def _decode_image(self, y_hat, q):
+    def _decode_image(self, y_hat, q, clamp=True):
+        """dec + refine; write mode clamps (image_model.py:251), estimate
+        mode returns refine's output unclamped (image_model.py:129-130)."""
         f = y_hat
         for b in self.d1:
             f = b(f)
         f = self.d1u(f, scale=q)
         f = self.d2u(self.d2(f))
         f = self.refine_unet(f)
-        return K.conv(self.refine_conv, f, out_dtype=F32, act=ACT_CLAMP01)
+        return K.conv(self.refine_conv, f, out_dtype=F32, act=ACT_CLAMP01 if clamp else K.ACT_NONE)
 
-    def compress(self, x, q_in_ckpt, q_index):
-        """image_model.py:198-229 (without the unused encoder recon)."""
-        x = as_act(x)
-        q_enc, _ = self.get_q_for_inference(q_in_ckpt, q_index)
+    def _analysis(self, x, q_enc):
+        """IntraEncoder + hyper encoder: (y, z_hat)."""
         f = self.e1(x)
         f = self.e1b(f, scale=q_enc)
         for b in self.e2:
             f = b(f)
         y = K.conv(self.e2c, f, out_dtype=F32)
-        yh, yw = y.H, y.W
         z = self.he0(pad_for_y(y))
         z = K.conv(self.he1, z, act=ACT_LRELU, slope=0.01)
-        z_hat = K.conv(self.he3, z, act=K.ACT_ROUND)
+        return y, K.conv(self.he3, z, act=K.ACT_ROUND)
+
+    def forward(self, x, q_in_ckpt=False, q_index=None):
+        """Estimate mode, image_model.py:114-149: Gaussian bits for y,
+        factorized bits for z, summed on the GPU."""
+        x = as_act(x)
+        q_enc, q_dec = self.get_q_for_inference(q_in_ckpt, q_index)
+        y, z_hat = self._analysis(x, q_enc)
+        bc = BitCounter(self.dev, ("y", "z"))
+        bc.factorized("z", z_hat, self.z_table)
+        params = self._params(z_hat, y.H, y.W)
+        y_hat = self.prior.estimate(y, params, bc.buffer("y", self.N * y.H * y.W), True)
+        x_hat = self._decode_image(y_hat, q_dec, clamp=False)
+        r = bits_result(bc.totals(), x.H * x.W, ("y", "z"))
+        return {"x_hat": x_hat.nchw_view(), "bit": r["bit"], "bpp": r["bpp"], "bpp_y": r["bpp_y"],
+                "bpp_z": r["bpp_z"]}
+
+    def compress(self, x, q_in_ckpt, q_index):
+        """image_model.py:198-229 (without the unused encoder recon)."""
+        x = as_act(x)
+        q_enc, _ = self.get_q_for_inference(q_in_ckpt, q_index)
+        y, z_hat = self._analysis(x, q_enc)
+        yh, yw = y.H, y.W
         params = self._params(z_hat, yh, yw)
         sb = SymbolBuffer(self.dev)
         c_z = sb.plan("z", self.N * z_hat.H * z_hat.W)
@@ -155,9 +176,11 @@ class IntraNoAR:
         return {"x_hat": self._decode_image(y_hat, q_dec)}
 
     def encode_decode(self, x, q_in_ckpt, q_index, output_path=None, pic_width=None, pic_height=None):
-        """image_model.py:169-196 (write mode)."""
+        """image_model.py:169-196: write mode, or estimate mode when
+        output_path is None."""
         if output_path is None:
-            raise NotImplementedError("estimate mode is not implemented on the GPU path; pass output_path")
+            enc = self.forward(x, q_in_ckpt, q_index)
+            return {"bit": enc["bit"], "x_hat": enc["x_hat"]}
         assert pic_height is not None and pic_width is not None
         enc = self.compress(x, q_in_ckpt, q_index)
         encode_i(pic_height, pic_width, q_in_ckpt, q_index, enc["bit_stream"], output_path)

@@ -5,8 +5,8 @@ ec_thread, stream_part, inplace)``, ``load_state_dict``, ``update``,
 ``get_q_scales_from_ckpt``, ``compress``, ``decompress``, ``encode_decode``.
 Frames and DPB entries are NHWC ``Act`` views on the GPU (``x`` may also be
 passed as a (1, 3, H, W) tensor).  Write mode (``output_path`` given) is the
-real-bitstream path; estimate mode is not implemented on the GPU yet and
-raises.  The encoder skips compress()'s dead reconstruction
+real-bitstream path; ``output_path=None`` runs estimate mode
+(``forward_one_frame``) with the bits summed on the GPU.  The encoder skips compress()'s dead reconstruction
 (video_model.py:468), whose output the reference discards in write mode.
 """
 import time
@@ -19,7 +19,7 @@ from ..layers import (Ctx, Precision, DepthConvBlock, ResidualBlockWithStride, R
                       ResBlock, UNet, SpyNet, Grids, hyper_enc, hyper_dec, cast)
 from ..entropy import ScaleTable, FactorizedTable, EntropyCoder
 from ..stream_helper import (get_downsampled_shape, encode_p, decode_p, filesize, get_state_dict)
-from .common import SymbolBuffer, QuadtreePrior, pad_for_y, crop_to, q_fine, curr_q
+from .common import SymbolBuffer, QuadtreePrior, BitCounter, bits_result, pad_for_y, crop_to, q_fine, curr_q
 
 G1, G2, G4, G8, G16 = 48, 64, 96, 96, 128  # video_model.py:19-23
 
@@ -382,12 +382,43 @@ class DMC:
         return {"dpb": {"ref_frame": x_hat.nchw_view(), "ref_feature": feature, "ref_mv_feature": mv_feature,
                         "ref_y": y_hat, "ref_mv_y": mv_y_hat}}
 
+    def forward_one_frame(self, x, dpb, q_in_ckpt=False, q_index=None, frame_idx=0):
+        """Estimate mode, video_model.py:559-628: the encoder graph with the
+        four-part prior run in estimate form, the reconstruction, and the
+        estimated bits (Laplace bits for y / mv_y, factorized bits for z /
+        mv_z) summed on the GPU.  Returns the reference's dict with Python
+        floats for the bpp / bit entries."""
+        x = as_act(x)
+        dpb = dpb_in(dpb)
+        mv_q_enc, mv_q_dec, y_q_enc, y_q_dec = self.get_q_for_inference(q_in_ckpt, q_index)
+        bc = BitCounter(self.dev, ("mv_y", "mv_z", "y", "z"))
+        est_mv = self.optic_flow(x, dpb["ref_frame"])
+        mv_y = self._mv_encoder(est_mv, dpb["ref_mv_feature"], mv_q_enc)
+        yh, yw = mv_y.H, mv_y.W
+        mv_z_hat = self.mv_henc(pad_for_y(mv_y))
+        bc.factorized("mv_z", mv_z_hat, self.mvz_table)
+        mv_params = self._mv_prior_params(mv_z_hat, dpb, yh, yw)
+        mv_y_hat = self.mv_prior.estimate(mv_y, mv_params, bc.buffer("mv_y", 64 * yh * yw), False)
+        mv_hat, mv_feature = self._mv_decoder(mv_y_hat, mv_q_dec)
+        c1, c2, c3 = self._motion_compensation(dpb, mv_hat, frame_idx)
+        y = self._contextual_encoder(x, c1, c2, c3, y_q_enc)
+        z_hat = self.y_henc(pad_for_y(y))
+        bc.factorized("z", z_hat, self.z_table)
+        params = self._res_prior_params(z_hat, dpb, c3, yh, yw)
+        y_hat = self.y_prior.estimate(y, params, bc.buffer("y", G16 * yh * yw), False)
+        x_hat, feature = self._recon(y_hat, c1, c2, c3, y_q_dec)
+        out = bits_result(bc.totals(), x.H * x.W, ("mv_y", "mv_z", "y", "z"))
+        out["dpb"] = {"ref_frame": x_hat.nchw_view(), "ref_feature": feature, "ref_mv_feature": mv_feature,
+                      "ref_y": y_hat, "ref_mv_y": mv_y_hat}
+        return out
+
     def encode_decode(self, x, dpb, q_in_ckpt, q_index, output_path=None, pic_width=None, pic_height=None,
                       frame_idx=0):
-        """video_model.py:522-557 (write mode)."""
+        """video_model.py:522-557: write mode (output_path given: real
+        bitstream through a file, bit = filesize * 8) or estimate mode."""
         if output_path is None:
-            raise NotImplementedError("estimate mode (forward_one_frame) is not implemented on the GPU path; "
-                                      "pass output_path for the real-bitstream path")
+            enc = self.forward_one_frame(x, dpb, q_in_ckpt=q_in_ckpt, q_index=q_index, frame_idx=frame_idx)
+            return {"dpb": enc["dpb"], "bit": enc["bit"], "encoding_time": 0, "decoding_time": 0}
         torch.cuda.synchronize(self.dev)
         t0 = time.time()
         enc = self.compress(x, dpb, q_in_ckpt, q_index, frame_idx)

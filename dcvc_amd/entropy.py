@@ -91,6 +91,22 @@ class FactorizedTable:
         self.sizes, self.offsets = (length + 2).int().numpy(), (-lo).int().numpy()
         self.table = CdfTable(self.cdf, self.sizes, self.offsets)
         self.channel = channel
+        # per-channel constants of the Bitparm chain for estimate-mode bits
+        # (dcvc_factorized_bits): softplus(h), b, tanh(a) per layer, in fp32
+        # with the reference's own torch ops
+        cols = []
+        for i in range(1, 5):
+            q = f"{prefix}.f{i}"
+            cols += [F.softplus(P[q + ".h"]).reshape(-1), P[q + ".b"].reshape(-1)]
+            if i < 4:
+                cols.append(torch.tanh(P[q + ".a"]).reshape(-1))
+        self.chain = torch.stack(cols, dim=1).float().contiguous()  # [C][11]
+        self._chain_dev = {}
+
+    def chain_on(self, device):
+        if device not in self._chain_dev:
+            self._chain_dev[device] = self.chain.to(device)
+        return self._chain_dev[device]
 
     def indexes(self, h, w):
         """BitEstimator.build_indexes (entropy_models.py:179-183), NCHW order."""

@@ -69,6 +69,9 @@ HIP_SYMBOLS = [
     ("dcvc_quadtree_decode_step", _i, [_T, _T, _i, _vp, _T, _T, _vp]),
     ("dcvc_nhwc_to_symbols", _i, [_T, _vp, _vp]),
     ("dcvc_symbols_to_nhwc", _i, [_vp, _T, _vp]),
+    ("dcvc_quadtree_estimate_step", _i, [_T, _T, _T, _i, _T, _T, _vp, _i, _vp]),
+    ("dcvc_factorized_bits", _i, [_T, _vp, _vp, _vp]),
+    ("dcvc_sum_f32", _i, [_vp, ctypes.c_int64, _vp, _vp]),
 ]
 
 _L = None
@@ -370,3 +373,19 @@ def to_symbols(x, sym):
 
 def from_symbols(sym, y):
     check(lib().dcvc_symbols_to_nhwc(sym.data_ptr(), y.c(), stream()), "symbols_to_nhwc")
+
+
+def qt_estimate_step(y, params, sm, k, yhs, yhat, bits, gaussian):
+    check(lib().dcvc_quadtree_estimate_step(y.c(), params.c(), sm.c() if sm is not None else NULL_T, k,
+                                            yhs.c(), yhat.c(), bits.data_ptr(), 1 if gaussian else 0, stream()),
+          "quadtree_estimate_step")
+
+
+def factorized_bits(z, table, bits):
+    check(lib().dcvc_factorized_bits(z.c(), table.data_ptr(), bits.data_ptr(), stream()), "factorized_bits")
+
+
+def sum_f32(x, out):
+    """out (1-element fp32 device tensor) = fixed-order sum of x (fp32 device tensor)."""
+    check(lib().dcvc_sum_f32(x.data_ptr(), x.numel(), out.data_ptr(), stream()), "sum_f32")
+    return out

@@ -197,6 +197,30 @@ int dcvc_quadtree_decode_step(dcvc_tensor params, dcvc_tensor sm, int k,
 int dcvc_nhwc_to_symbols(dcvc_tensor x, int16_t *symbols, void *stream);
 int dcvc_symbols_to_nhwc(const int16_t *symbols, dcvc_tensor y, void *stream);
 
+/*
+ * Estimate mode (forward_one_frame), the bit counts the reference computes
+ * instead of coding (DCVC-DC/src/models/common_model.py:39-61,
+ * video_model.py:559-628, image_model.py:116-147).
+ * dcvc_quadtree_estimate_step: step k of forward_four_part_prior
+ * (common_model.py:142-252, write=False) — the y_hat outputs of
+ * dcvc_quadtree_encode_step plus, per coded element (same order as its
+ * symbols), bits = probs_to_bits(cdf(y_q + 0.5) - cdf(y_q - 0.5)) with
+ * sigma = clamp(scale, 1e-5, 1e10), Laplace (gaussian = 0, get_y_laplace_bits)
+ * or Normal (gaussian = 1, get_y_gaussian_bits).
+ */
+int dcvc_quadtree_estimate_step(dcvc_tensor y, dcvc_tensor params,
+                                dcvc_tensor sm, int k, dcvc_tensor yhs,
+                                dcvc_tensor yhat, float *bits, int gaussian,
+                                void *stream);
+/* get_z_bits (common_model.py:59-61): per element of the NHWC z_hat (fp32),
+ * bits of BitEstimator.get_cdf(z + 0.5) - get_cdf(z - 0.5) into bits[]
+ * (NHWC order).  table: [C][11] fp32 = softplus(h1), b1, tanh(a1), ...,
+ * softplus(h3), b3, tanh(a3), softplus(h4), b4 (entropy_models.py:56-122). */
+int dcvc_factorized_bits(dcvc_tensor z, const float *table, float *bits,
+                         void *stream);
+/* Deterministic (fixed-order) sum of n device floats into *out (device). */
+int dcvc_sum_f32(const float *x, int64_t n, float *out, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -153,3 +153,77 @@ def test_fast_bf16_latent_vs_oracle(dc_golden, oracle_runs, tag):
     stats = compare(run_product(dc_golden, tag, Precision.fast(latent_compute=BF16)), oracle_runs[tag])
     _dump(f"fast_bf16lat_{tag}", stats)
     check(stats, FAST_TOL)
+
+
+@pytest.fixture(scope="module")
+def oracle_est(dc_golden):
+    """Oracle estimate-mode runs (pinned bit-exact to the reference's
+    forward_one_frame / IntraNoAR.forward by tests/test_oracle_dc.py)."""
+    from oracle import dc_oracle as O
+    from oracle import rans_oracle as R
+    i = O.IntraOracle(dc_golden.i_state_dict(), R.pmf_to_quantized_cdf)
+    p = O.DMCOracle(dc_golden.p_state_dict(), R.pmf_to_quantized_cdf)
+    runs = {}
+    with torch.no_grad():
+        for tag in ("A", "B"):
+            meta = dc_golden.meta[tag]
+            frames, dpb = [], None
+            for t in range(meta["frames"]):
+                x, xp = dc_golden.frame_tensor(tag, t)
+                if t == 0:
+                    bit, xh = i.forward(xp, False, meta["q_index"])
+                    dpb = {"ref_frame": xh, "ref_feature": None, "ref_mv_feature": None, "ref_y": None,
+                           "ref_mv_y": None}
+                else:
+                    bit, dpb = p.forward_one_frame(xp, dpb, False, meta["q_index"], t % 4)
+                rec = dpb["ref_frame"].clamp_(0, 1)[:, :, :meta["h"], :meta["w"]]
+                frames.append({"bit": bit, "psnr": psnr(rec, x)})
+            runs[tag] = frames
+    return runs
+
+
+def run_product_estimate(dc_golden, tag, prec):
+    """The harness loop (test_video.py:108-167) with output_path=None."""
+    from dcvc_amd.dc import DMC, IntraNoAR
+    meta = dc_golden.meta[tag]
+    h, w, q = meta["h"], meta["w"], meta["q_index"]
+    inet = IntraNoAR(precision=prec).load_state_dict(dc_golden.i_state_dict())
+    pnet = DMC(precision=prec).load_state_dict(dc_golden.p_state_dict())
+    inet.update(force=True)
+    pnet.update(force=True)
+    out, dpb = [], None
+    for t in range(meta["frames"]):
+        x, xp = dc_golden.frame_tensor(tag, t)
+        xp = xp.cuda()
+        if t == 0:
+            r = inet.encode_decode(xp, False, q)
+            dpb = {"ref_frame": r["x_hat"], "ref_feature": None, "ref_mv_feature": None, "ref_y": None,
+                   "ref_mv_y": None}
+        else:
+            r = pnet.encode_decode(xp, dpb, False, q, frame_idx=t % 4)
+            dpb = r["dpb"]
+        assert isinstance(r["bit"], float)
+        recon = dpb["ref_frame"].clamp_(0, 1)
+        rec = recon[:, :, :h, :w].cpu()
+        out.append({"bit": r["bit"], "psnr": psnr(rec, x)})
+    return out
+
+
+@pytest.mark.parametrize("mode", ["parity", "fast"])
+@pytest.mark.parametrize("tag", ["B", "A"])
+def test_estimate_mode_vs_reference(dc_golden, oracle_est, tag, mode):
+    """Estimate mode (forward_one_frame / IntraNoAR.forward) on the GPU:
+    estimated bits against the reference's own numbers (golden fixtures),
+    reconstruction PSNR against the pinned oracle."""
+    from dcvc_amd.layers import Precision
+    prec = Precision.parity() if mode == "parity" else Precision.fast()
+    tol = PARITY_TOL if mode == "parity" else FAST_TOL
+    prod = run_product_estimate(dc_golden, tag, prec)
+    stats = []
+    for t, (a, b) in enumerate(zip(prod, oracle_est[tag])):
+        ref_bit = dc_golden.meta[tag]["est"][t]["bit"]
+        stats.append({"t": t, "bit": a["bit"], "bit_ref": ref_bit, "psnr": a["psnr"], "psnr_oracle": b["psnr"]})
+    _dump(f"estimate_{mode}_{tag}", stats)
+    for s in stats:
+        assert abs(s["bit"] - s["bit_ref"]) / s["bit_ref"] <= tol["bits_rel"], s
+        assert abs(s["psnr"] - s["psnr_oracle"]) <= tol["psnr_db"], s
