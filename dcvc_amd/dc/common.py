@@ -14,8 +14,9 @@ class SymbolBuffer:
     symbols (and indexes) land in one device buffer that is copied to pinned
     host memory with a single transfer."""
 
-    def __init__(self, device):
+    def __init__(self, device, sym_dtype=torch.int16):
         self.dev = device
+        self.sym_dtype = sym_dtype  # int16 (DC coder) or int32 (HEM coder)
         self.sizes = []
         self.kinds = []
 
@@ -26,7 +27,7 @@ class SymbolBuffer:
 
     def alloc(self):
         total = int(sum(self.sizes))
-        self.sym = torch.empty(total, dtype=torch.int16, device=self.dev)
+        self.sym = torch.empty(total, dtype=self.sym_dtype, device=self.dev)
         self.idx = torch.empty(total, dtype=torch.int16, device=self.dev)
         self.offs = np.concatenate([[0], np.cumsum(self.sizes)]).astype(np.int64)
         return self
@@ -38,7 +39,7 @@ class SymbolBuffer:
         return self.idx[self.offs[i]:self.offs[i + 1]]
 
     def to_host(self):
-        s = torch.empty(self.sym.numel(), dtype=torch.int16, pin_memory=True)
+        s = torch.empty(self.sym.numel(), dtype=self.sym_dtype, pin_memory=True)
         x = torch.empty(self.idx.numel(), dtype=torch.int16, pin_memory=True)
         s.copy_(self.sym, non_blocking=True)
         x.copy_(self.idx, non_blocking=True)
@@ -64,7 +65,7 @@ class QuadtreePrior:
 
     def new_buffer(self, h, w):
         buf = K.empty(h, w, 4 * self.C, F32, self.ctx.dev)
-        buf.buf[:, :, :self.C].zero_()
+        K.fill(buf.ch(0, self.C), 0.0)  # y_hat_so_far starts at zero
         return buf
 
     def step_params(self, buf, k):

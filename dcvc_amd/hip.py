@@ -72,6 +72,16 @@ HIP_SYMBOLS = [
     ("dcvc_quadtree_estimate_step", _i, [_T, _T, _T, _i, _T, _T, _vp, _i, _vp]),
     ("dcvc_factorized_bits", _i, [_T, _vp, _vp, _vp]),
     ("dcvc_sum_f32", _i, [_vp, ctypes.c_int64, _vp, _vp]),
+    ("dcvc_dual_prior_encode_step", _i, [_T, _T, _T, _i, _T, _vp, _vp, _vp, _f, _f, _vp]),
+    ("dcvc_dual_prior_indexes_step", _i, [_T, _T, _i, _vp, _f, _f, _vp]),
+    ("dcvc_dual_prior_decode_step", _i, [_T, _T, _i, _vp, _T, _vp, _vp]),
+    ("dcvc_dual_prior_estimate_step", _i, [_T, _T, _T, _i, _T, _vp, _vp, _i, _f, _vp]),
+    ("dcvc_channel_div", _i, [_T, _vp, _T, _vp]),
+    ("dcvc_fill", _i, [_T, _f, _vp]),
+    ("dcvc_nhwc_to_symbols_i32", _i, [_T, _vp, _vp]),
+    ("dcvc_symbols_i32_to_nhwc", _i, [_vp, _T, _vp]),
+    ("dcvc_se_scale", _i, [_T, _vp, _vp, _i, _vp, _vp, _vp]),
+    ("dcvc_se_apply", _i, [_T, _T, _vp, _T, _vp]),
 ]
 
 _L = None
@@ -389,3 +399,63 @@ def sum_f32(x, out):
     """out (1-element fp32 device tensor) = fixed-order sum of x (fp32 device tensor)."""
     check(lib().dcvc_sum_f32(x.data_ptr(), x.numel(), out.data_ptr(), stream()), "sum_f32")
     return out
+
+
+# ---- DCVC-HEM (hem.hip)
+def _ptr(t):
+    return t.data_ptr() if t is not None else None
+
+
+def dp_encode_step(y, buf, sm, k, yhat, post, sym, idx, log_min, log_step):
+    check(lib().dcvc_dual_prior_encode_step(y.c(), buf.c(), sm.c() if sm is not None else NULL_T, k, yhat.c(),
+                                            _ptr(post), sym.data_ptr(), idx.data_ptr(), log_min, log_step,
+                                            stream()), "dual_prior_encode_step")
+
+
+def dp_indexes_step(buf, sm, k, idx, log_min, log_step):
+    check(lib().dcvc_dual_prior_indexes_step(buf.c(), sm.c() if sm is not None else NULL_T, k, idx.data_ptr(),
+                                             log_min, log_step, stream()), "dual_prior_indexes_step")
+
+
+def dp_decode_step(buf, sm, k, sym, yhat, post):
+    check(lib().dcvc_dual_prior_decode_step(buf.c(), sm.c() if sm is not None else NULL_T, k, sym.data_ptr(),
+                                            yhat.c(), _ptr(post), stream()), "dual_prior_decode_step")
+
+
+def dp_estimate_step(y, buf, sm, k, yhat, post, bits, gaussian, scale_min):
+    check(lib().dcvc_dual_prior_estimate_step(y.c(), buf.c(), sm.c() if sm is not None else NULL_T, k, yhat.c(),
+                                              _ptr(post), bits.data_ptr(), 1 if gaussian else 0, scale_min,
+                                              stream()), "dual_prior_estimate_step")
+
+
+def channel_div(x, q, y=None):
+    if y is None:
+        y = empty(x.H, x.W, x.C, F32, x.buf.device)
+    check(lib().dcvc_channel_div(x.c(), q.data_ptr(), y.c(), stream()), "channel_div")
+    return y
+
+
+def to_symbols_i32(x, sym):
+    check(lib().dcvc_nhwc_to_symbols_i32(x.c(), sym.data_ptr(), stream()), "nhwc_to_symbols_i32")
+
+
+def from_symbols_i32(sym, y):
+    check(lib().dcvc_symbols_i32_to_nhwc(sym.data_ptr(), y.c(), stream()), "symbols_i32_to_nhwc")
+
+
+def se_scale(x, w1, w2, work, out):
+    check(lib().dcvc_se_scale(x.c(), w1.data_ptr(), w2.data_ptr(), w1.shape[0], work.data_ptr(), out.data_ptr(),
+                              stream()), "se_scale")
+    return out
+
+
+def se_apply(a, x, scale, y=None):
+    if y is None:
+        y = empty(a.H, a.W, a.C, a.dtype, a.buf.device)
+    check(lib().dcvc_se_apply(a.c(), x.c(), scale.data_ptr(), y.c(), stream()), "se_apply")
+    return y
+
+
+def fill(y, value=0.0):
+    check(lib().dcvc_fill(y.c(), float(value), stream()), "fill")
+    return y

@@ -62,17 +62,24 @@ class Ctx:
         if unused:
             raise RuntimeError(f"unexpected key(s) in state_dict: {sorted(unused)[:8]}")
 
-    def conv(self, name, stride=1, latent=False, compute=None, cin_pad=None):
+    def conv(self, name, stride=1, latent=False, compute=None, cin_pad=None, out_perm=None):
         """cin_pad: zero-pad the input channels to this count, for inputs whose
         concat buffer carries zero channels up to an 8-channel multiple (the
         kernels' 16-byte staging path); the products of the pad are exact
-        zeros, so the result is unchanged."""
+        zeros, so the result is unchanged.  out_perm: output channel order
+        (a permutation of the reference's), so a producer can write a
+        consumer's concat layout directly; per-channel results are unchanged."""
         if compute is None:
             compute = self.prec.latent_compute if latent else self.prec.feat_compute
         b = self.take(name + ".bias") if name + ".bias" in self.sd else None
         w = self.take(name + ".weight")
         if cin_pad is not None and cin_pad > w.shape[1]:
             w = torch.nn.functional.pad(w.detach().float(), (0, 0, 0, 0, 0, cin_pad - w.shape[1]))
+        if out_perm is not None:
+            perm = torch.as_tensor(out_perm, dtype=torch.long)
+            w = w.detach().float()[perm]
+            if b is not None:
+                b = b.detach().float()[perm]
         return K.ConvW(w, b, stride, compute, self.dev)
 
     def dw(self, name):

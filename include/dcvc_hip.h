@@ -221,6 +221,56 @@ int dcvc_factorized_bits(dcvc_tensor z, const float *table, float *bits,
 /* Deterministic (fixed-order) sum of n device floats into *out (device). */
 int dcvc_sum_f32(const float *x, int64_t n, float *out, void *stream);
 
+/*
+ * DCVC-HEM dual (checkerboard) prior, DCVC-HEM/src/models/common_model.py:
+ * 84-188 (forward/compress/decompress_dual_prior).  buf: the spatial prior's
+ * fp32 input [y_hat_0_0 | y_hat_1_1 (C) | means | scales | quant_step], 4C
+ * channels, written by the caller's prior fusion (params) and by step 0
+ * (y_hat part); sm: the spatial prior's output [scales_0 | means_0 |
+ * scales_1 | means_1] for k = 1 (NULL ptr for k = 0).  Step k writes, per
+ * site of its checkerboard half, int32 symbols / int16 CDF indexes in the
+ * NCHW order of y_q_w_k (C/2 channels), and y_hat * quant_step into yhat.
+ */
+int dcvc_dual_prior_encode_step(dcvc_tensor y, dcvc_tensor buf, dcvc_tensor sm,
+                                int k, dcvc_tensor yhat,
+                                const float *post_scale, int32_t *symbols,
+                                int16_t *indexes, float log_min,
+                                float log_step, void *stream);
+int dcvc_dual_prior_indexes_step(dcvc_tensor buf, dcvc_tensor sm, int k,
+                                 int16_t *indexes, float log_min,
+                                 float log_step, void *stream);
+int dcvc_dual_prior_decode_step(dcvc_tensor buf, dcvc_tensor sm, int k,
+                                const int32_t *symbols, dcvc_tensor yhat,
+                                const float *post_scale, void *stream);
+/* Estimate form (write=False): per-site bits, Laplace (gaussian = 0) or
+ * Normal (gaussian = 1) with sigma clamped to [scale_min, 1e10]
+ * (get_y_laplace_bits 1e-5 / get_y_gaussian_bits 0.11, common_model.py:58-70). */
+int dcvc_dual_prior_estimate_step(dcvc_tensor y, dcvc_tensor buf,
+                                  dcvc_tensor sm, int k, dcvc_tensor yhat,
+                                  const float *post_scale, float *bits,
+                                  int gaussian, float scale_min, void *stream);
+/* post_scale (nullable, [C] fp32): yhat = (y_hat * quant_step) * post_scale,
+ * the caller's y_hat * curr_q (video_model.py:278-279, 302-303) fused in. */
+/* y[..] = value (a channel window of a concat buffer: the reference's
+ * torch.zeros_like stand-ins for an absent ref_y / ref_mv_y). */
+int dcvc_fill(dcvc_tensor y, float value, void *stream);
+/* y = x / q[c], fp32 (y / curr_q, video_model.py:270, 289). */
+int dcvc_channel_div(dcvc_tensor x, const float *q, dcvc_tensor y, void *stream);
+/* HEM factorized symbols: int32, no clamp (BitEstimator.encode /
+ * decode_stream, DCVC-HEM/src/entropy_models/entropy_models.py:182-195). */
+int dcvc_nhwc_to_symbols_i32(dcvc_tensor x, int32_t *symbols, void *stream);
+int dcvc_symbols_i32_to_nhwc(const int32_t *symbols, dcvc_tensor y,
+                             void *stream);
+/* SELayer (DCVC-HEM/src/models/video_net.py:157-170): scale_out[c] =
+ * sigmoid(W2 relu(W1 mean_hw(x)))[c]; w1 [reduced][C], w2 [C][reduced]
+ * fp32 (nn.Linear, no bias); work: >= 256 * C floats of device scratch. */
+int dcvc_se_scale(dcvc_tensor x, const float *w1, const float *w2, int reduced,
+                  float *work, float *scale_out, void *stream);
+/* y = a + x * scale[c] (ConvBlockResidual: up_dim(x) + SE(x1),
+ * video_net.py:185-188). */
+int dcvc_se_apply(dcvc_tensor a, dcvc_tensor x, const float *scale,
+                  dcvc_tensor y, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -49,3 +49,20 @@ def test_strict_rejects_unknown_key(stub):
     sd["not_a_layer.weight"] = torch.zeros(1)
     with pytest.raises(RuntimeError):
         DMC(device=torch.device("cpu")).load_state_dict(sd)
+
+
+def _hem_sd(kind):
+    spec = json.load(open(SPEC.replace("dc_param_spec", "hem_param_spec")))[kind]
+    return synthetic_state_dict([(n, tuple(s)) for n, s in spec], seed=0)
+
+
+def test_hem_dmc_consumes_reference_state_dict(stub):
+    from dcvc_amd.hem import DMC
+    m = DMC(device=torch.device("cpu")).load_state_dict(_hem_sd("inter"))
+    assert m.ce_c4.cout == 96 and m.y_fusion.c0.cin == 480 and m.y_prior.spatial.c4.cout == 192
+
+
+def test_hem_intra_consumes_reference_state_dict(stub):
+    from dcvc_amd.hem import IntraNoAR
+    m = IntraNoAR(device=torch.device("cpu")).load_state_dict(_hem_sd("intra"))
+    assert m.enc.last.cout == 192 and m.prior.spatial.c0.cin == 768
