@@ -1,5 +1,7 @@
 """DCVC-DC encode+decode throughput on MI355X (BASELINE.json metric, config C3:
 DCVC-DC RGB 1920x1080, padded to 1088, IP=32, write mode = real bitstreams).
+``--model hem`` runs config C2 instead (DCVC-HEM 1920x1080, zero-padded to
+1088, IP=32, the loop of DCVC-HEM/test_video.py:108-160).
 
 One step = one frame through ``encode_decode(..., output_path=...)``: the
 I-frame codec when frame_idx % gop == 0, else the P-frame codec, exactly the
@@ -32,6 +34,10 @@ PEAK_HBM_GBS = 8000.0
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--model", choices=["dc", "hem"], default="dc",
+                    help="dc = DCVC-DC (config C3, the 30 fps target); hem = DCVC-HEM (config C2)")
+    ap.add_argument("--rate", type=int, default=0,
+                    help="HEM rate point: index into the checkpoint's q_scale ladders (test_video.py:274-300)")
     ap.add_argument("--steps", type=int, default=32)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--height", type=int, default=1080)
@@ -47,20 +53,27 @@ def parse():
     return ap.parse_args()
 
 
-def spec():
-    with open(os.path.join(HERE, "dcvc_amd", "data", "dc_param_spec.json")) as f:
+HEM_GAIN = 1.6   # tests/golden/make_golden_hem.py: latents beyond 0/+-1 without blow-up
+
+
+def spec(model="dc"):
+    with open(os.path.join(HERE, "dcvc_amd", "data", f"{model}_param_spec.json")) as f:
         d = json.load(f)
     return [(n, tuple(s)) for n, s in d["intra"]], [(n, tuple(s)) for n, s in d["inter"]]
 
 
-def make_weights(dist, rank, device):
+def make_weights(dist, rank, device, model="dc"):
     """Rank 0 builds the state dicts; one RCCL broadcast of the flat blob."""
     from dcvc_amd.weights import synthetic_state_dict
-    i_spec, p_spec = spec()
+    i_spec, p_spec = spec(model)
     names = [("i", n, s) for n, s in i_spec] + [("p", n, s) for n, s in p_spec]
     total = sum(int(np.prod(s)) for _, _, s in names)
     if rank == 0:
-        isd, psd = synthetic_state_dict(i_spec, seed=0), synthetic_state_dict(p_spec, seed=1)
+        if model == "hem":
+            isd = synthetic_state_dict(i_spec, seed=0, gain=HEM_GAIN)
+            psd = synthetic_state_dict(p_spec, seed=1, gain=HEM_GAIN)
+        else:
+            isd, psd = synthetic_state_dict(i_spec, seed=0), synthetic_state_dict(p_spec, seed=1)
         flat = torch.cat([(isd if k == "i" else psd)[n].reshape(-1) for k, n, _ in names]).to(device)
     else:
         flat = torch.empty(total, dtype=torch.float32, device=device)
@@ -138,6 +151,55 @@ def cpu_baseline(isd, psd, args):
                       f"scaled x{area:.1f} by area to 1088x1920, GOP {gop} average"}
 
 
+def hem_q(sd_i, sd_p, rate):
+    """(i q_scale, mv_y q_scale, y q_scale) of rate point `rate` from the
+    checkpoints' ladders, as DCVC-HEM/test_video.py:274-300 picks them."""
+    return (float(sd_i["q_scale"].reshape(-1)[rate]), float(sd_p["mv_y_q_scale"].reshape(-1)[rate]),
+            float(sd_p["y_q_scale"].reshape(-1)[rate]))
+
+
+def cpu_baseline_hem(isd, psd, args):
+    """HEM oracle on the same bounded sample as cpu_baseline (one I-frame
+    untimed-ready, one P-frame, write mode, per-call rANS encode+decode)."""
+    from oracle import hem_oracle as O
+    from oracle import rans_oracle as R
+    from dcvc_amd.synth import moving_pattern, to_float
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    h, w = 512, 960
+    inet = O.IntraOracle(isd, R.pmf_to_quantized_cdf)
+    pnet = O.DMCOracle(psd, R.pmf_to_quantized_cdf)
+    tabs = {"i_y": inet.tab_y[:3], "i_z": inet.tab_z[:3], "p_y": pnet.tab_y[:3], "p_z": pnet.tab_z[:3],
+            "p_mvz": pnet.tab_mvz[:3]}
+    qi, qmv, qy = (round(q * 100) / 100 for q in hem_q(isd, psd, args.rate))
+
+    def coder(calls):
+        pos = [0]
+
+        def decoder(kind, idx):
+            sym = calls[pos[0]][1]
+            pos[0] += 1
+            st = R.hem_encode(sym.to(torch.int32).numpy(), idx.numpy(), *tabs[kind])
+            return torch.from_numpy(R.hem_decode(st, idx.numpy(), *tabs[kind]).astype(np.int64))
+        return decoder
+
+    frames = [torch.from_numpy(to_float(moving_pattern(h, w, t, seed=1))).unsqueeze(0) for t in range(2)]
+    with torch.no_grad():
+        t0 = time.time()
+        xh = inet.decompress(coder(inet.compress(frames[0], qi)), h, w, qi)
+        t_i = time.time() - t0
+        dpb = {"ref_frame": xh, "ref_feature": None, "ref_y": None, "ref_mv_y": None}
+        t0 = time.time()
+        pnet.decompress(dpb, coder(pnet.compress(frames[1], dpb, qmv, qy)), h, w, qmv, qy)
+        t_p = time.time() - t0
+    area = (1088 * 1920) / (h * w)
+    gop = args.gop
+    fps = gop / (area * (t_i + (gop - 1) * t_p))
+    return {"value": fps, "unit": "frames/s", "cores": threads, "kind": "port",
+            "sample": f"HEM oracle write-mode I+P encode+decode at {h}x{w} (I {t_i:.1f}s, P {t_p:.1f}s), "
+                      f"scaled x{area:.2f} by area to 1088x1920, GOP {gop} average"}
+
+
 def pmc_traffic(kname):
     """HBM bytes per launch of `kname` (instantiation@grid, which fixes the
     launch geometry) from the committed rocprofv3 PMC summary
@@ -173,19 +235,27 @@ def main():
     torch.cuda.set_device(device)
 
     from dcvc_amd import hip as K
-    from dcvc_amd.dc import DMC, IntraNoAR
     from dcvc_amd.layers import Precision
     from dcvc_amd.synth import moving_pattern
 
-    isd, psd = make_weights(dist, rank, device)
+    hem = args.model == "hem"
+    isd, psd = make_weights(dist, rank, device, args.model)
     prec = Precision.fast(latent_compute=K.BF16) if args.precision == "fast" else Precision.parity()
-    inet = IntraNoAR(precision=prec, stream_part=args.stream_part, device=device).load_state_dict(isd)
-    pnet = DMC(precision=prec, stream_part=args.stream_part, device=device).load_state_dict(psd)
+    if hem:
+        from dcvc_amd.hem import DMC, IntraNoAR
+        inet = IntraNoAR(precision=prec, device=device).load_state_dict(isd)
+        pnet = DMC(precision=prec, device=device).load_state_dict(psd)
+        qi, qmv, qy = hem_q(isd, psd, args.rate)
+    else:
+        from dcvc_amd.dc import DMC, IntraNoAR
+        inet = IntraNoAR(precision=prec, stream_part=args.stream_part, device=device).load_state_dict(isd)
+        pnet = DMC(precision=prec, stream_part=args.stream_part, device=device).load_state_dict(psd)
     inet.update(force=True)
     pnet.update(force=True)
 
     h, w = args.height, args.width
-    H, W = (h + 15) // 16 * 16, (w + 15) // 16 * 16
+    align = 64 if hem else 16     # HEM test_video.py:113-119 pads to 64, DC to 16
+    H, W = (h + align - 1) // align * align, (w + align - 1) // align * align
     nframes = args.warmup + args.steps
     frames = [torch.from_numpy(moving_pattern(h, w, t, seed=shard_seed(rank))).to(device) for t in range(nframes)]
     out_dir = f"/dev/shm/dcvc_bench_{os.getpid()}"
@@ -196,9 +266,20 @@ def main():
     kinds = []
 
     def step(i):
-        K.frame_to_nhwc(frames[i], h, w, x)     # uint8 CHW -> padded NHWC (replicate), test_video.py:130
+        # uint8 CHW -> padded NHWC: replicate (DC test_video.py:130) / zeros (HEM)
+        K.frame_to_nhwc(frames[i], h, w, x, zero_pad=hem)
         path = os.path.join(out_dir, f"{i}.bin")
-        if i % args.gop == 0:
+        if hem:
+            if i % args.gop == 0:
+                r = inet.encode_decode(x, qi, path, pic_width=w, pic_height=h)
+                state["dpb"] = {"ref_frame": r["x_hat"], "ref_feature": None, "ref_y": None, "ref_mv_y": None}
+                kinds.append("I")
+            else:
+                r = pnet.encode_decode(x, state["dpb"], path, pic_width=w, pic_height=h,
+                                       mv_y_q_scale=qmv, y_q_scale=qy)
+                state["dpb"] = r["dpb"]
+                kinds.append("P")
+        elif i % args.gop == 0:
             r = inet.encode_decode(x, False, args.q_index, path, pic_width=w, pic_height=h)
             state["dpb"] = {"ref_frame": r["x_hat"], "ref_feature": None, "ref_mv_feature": None,
                             "ref_y": None, "ref_mv_y": None}
@@ -288,10 +369,11 @@ def main():
         tp = [p for p, k in zip(per, kinds[args.warmup:]) if k == "P"]
         cpu = None
         if not args.no_cpu_baseline and world == 1:
-            cpu = cpu_baseline(isd, psd, args)
+            cpu = cpu_baseline_hem(isd, psd, args) if hem else cpu_baseline(isd, psd, args)
         timed_bits = bits[args.warmup:nframes]
         line = {
-            "metric": "encode+decode fps @1080p per GPU (DCVC-DC write mode, real bitstreams)",
+            "metric": f"encode+decode fps @1080p per GPU ({'DCVC-HEM' if hem else 'DCVC-DC'} write mode, "
+                      "real bitstreams)",
             "value": round(world * args.steps / elapsed, 4),
             "unit": "frames/s",
             "n_gpus": world,
@@ -303,9 +385,11 @@ def main():
             "vs_baseline": None,
             "dtype": "bf16" if args.precision == "fast" else "f32",
             "data": "synthetic (moving sinusoid + noise frames, seeded random weights)",
-            "config": {"workload": f"C3 DCVC-DC RGB {w}x{h} (pad {W}x{H}) IP={args.gop} write mode",
-                       "gop": args.gop, "q_index": args.q_index, "precision": args.precision,
-                       "stream_part": args.stream_part, "parallelism": f"sequence-sharded x{world}",
+            "config": {"workload": (f"C2 DCVC-HEM RGB {w}x{h} (zero pad {W}x{H}) IP={args.gop} write mode"
+                                    if hem else f"C3 DCVC-DC RGB {w}x{h} (pad {W}x{H}) IP={args.gop} write mode"),
+                       "gop": args.gop, "precision": args.precision,
+                       **({"rate": args.rate, "q_scales": [round(qi, 4), round(qmv, 4), round(qy, 4)]} if hem
+                          else {"q_index": args.q_index, "stream_part": args.stream_part}), "parallelism": f"sequence-sharded x{world}",
                        "I_frames_timed": n_i,
                        "ms_I": round(1e3 * float(np.mean(ti)), 2) if ti else None,
                        "ms_P": round(1e3 * float(np.mean(tp)), 2) if tp else None,

@@ -182,11 +182,85 @@ __global__ void from_sym32_kernel(const int32_t *sym, View y) {
 // relu(W1 y)); out = a + x * s[c] (ConvBlockResidual's up_dim(x) + SE(x1),
 // :185-188).  The mean is a fixed-order two-stage sum (partial sums over
 // pixel ranges, then one block), so it is reproducible.
-constexpr int kSePart = 256;  // pixel ranges of the first stage
+constexpr int kSePart = 256;  // pixel ranges of the first stage (work = kSePart * C floats)
 
+// V consecutive channels of one pixel as floats (16-byte loads when V > 1).
+template <typename T, int V> struct VecLd;
+template <> struct VecLd<uint16_t, 8> {
+  __device__ __forceinline__ static void load(const void *p, int64_t i, float *v) {
+    const uint4 q = *reinterpret_cast<const uint4 *>(reinterpret_cast<const uint16_t *>(p) + i);
+    const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      v[2 * j] = __uint_as_float(w[j] << 16);
+      v[2 * j + 1] = __uint_as_float(w[j] & 0xffff0000u);
+    }
+  }
+  __device__ __forceinline__ static void store(void *p, int64_t i, const float *v) {
+    uint32_t w[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) w[j] = (uint32_t)f2bf(v[2 * j]) | ((uint32_t)f2bf(v[2 * j + 1]) << 16);
+    *reinterpret_cast<uint4 *>(reinterpret_cast<uint16_t *>(p) + i) = make_uint4(w[0], w[1], w[2], w[3]);
+  }
+};
+template <> struct VecLd<float, 4> {
+  __device__ __forceinline__ static void load(const void *p, int64_t i, float *v) {
+    const float4 q = *reinterpret_cast<const float4 *>(reinterpret_cast<const float *>(p) + i);
+    v[0] = q.x, v[1] = q.y, v[2] = q.z, v[3] = q.w;
+  }
+  __device__ __forceinline__ static void store(void *p, int64_t i, const float *v) {
+    *reinterpret_cast<float4 *>(reinterpret_cast<float *>(p) + i) = make_float4(v[0], v[1], v[2], v[3]);
+  }
+};
+template <typename T> struct VecLd<T, 1> {
+  __device__ __forceinline__ static void load(const void *p, int64_t i, float *v) { v[0] = ld<T>(p, i); }
+  __device__ __forceinline__ static void store(void *p, int64_t i, const float *v) { st<T>(p, i, v[0]); }
+};
+
+// Stage 1: block b sums pixels [b * n / kSePart, (b + 1) * n / kSePart).
+// Thread t owns channel vector t % CV of pixel lane t / CV (CV = C / V
+// vectors per pixel, lanes = 256 / CV pixels per iteration), so a wave reads
+// whole contiguous pixels; lanes are then folded in LDS in lane order.  The
+// summation order is fixed by (n, C), so the mean is reproducible.
+template <typename TX, int V>
+__global__ __launch_bounds__(256) void se_partial_kernel(View x, float *part) {
+  __shared__ float red[256 * V];
+  const int C = x.C, CV = C / V, lanes = 256 / CV;
+  const int t = threadIdx.x, lane = t / CV, cv = t - lane * CV;
+  const int64_t n = (int64_t)x.H * x.W;
+  const int64_t p0 = blockIdx.x * n / kSePart, p1 = (blockIdx.x + 1) * n / kSePart;
+  float a[V];
+#pragma unroll
+  for (int j = 0; j < V; ++j) a[j] = 0.f;
+  if (lane < lanes) {
+    int64_t p = p0 + lane;
+    for (; p + lanes < p1; p += 2 * lanes) {  // two pixels in flight per thread
+      float u[V], w[V];
+      VecLd<TX, V>::load(x.p, p * x.cs + x.co + cv * V, u);
+      VecLd<TX, V>::load(x.p, (p + lanes) * x.cs + x.co + cv * V, w);
+#pragma unroll
+      for (int j = 0; j < V; ++j) a[j] += u[j] + w[j];
+    }
+    if (p < p1) {
+      float u[V];
+      VecLd<TX, V>::load(x.p, p * x.cs + x.co + cv * V, u);
+#pragma unroll
+      for (int j = 0; j < V; ++j) a[j] += u[j];
+    }
+#pragma unroll
+    for (int j = 0; j < V; ++j) red[lane * C + cv * V + j] = a[j];
+  }
+  __syncthreads();
+  for (int c = t; c < C; c += 256) {
+    float s = 0.f;
+    for (int l = 0; l < lanes; ++l) s += red[l * C + c];
+    part[(int64_t)blockIdx.x * C + c] = s;
+  }
+}
+
+// Scalar fallback (channel views that are not 16-byte aligned, or C / V > 256).
 template <typename TX>
-__global__ void se_partial_kernel(View x, float *part) {
-  // block b: pixels [b * n / kSePart, (b + 1) * n / kSePart); thread c: channel c
+__global__ void se_partial_scalar_kernel(View x, float *part) {
   const int64_t n = (int64_t)x.H * x.W;
   const int64_t p0 = blockIdx.x * n / kSePart, p1 = (blockIdx.x + 1) * n / kSePart;
   for (int c = threadIdx.x; c < x.C; c += blockDim.x) {
@@ -198,13 +272,25 @@ __global__ void se_partial_kernel(View x, float *part) {
 
 __global__ void se_fc_kernel(const float *part, int C, int R, float inv_n, const float *w1, const float *w2,
                              float *s) {
-  __shared__ float mean[1024], hid[64];
-  for (int c = threadIdx.x; c < C; c += blockDim.x) {
-    float a = 0.f;
-    for (int b = 0; b < kSePart; ++b) a += part[b * C + c];
-    mean[c] = a * inv_n;
+  __shared__ float mean[1024], hid[64], red[1024];
+  // stage 2: 1024 threads = G groups of C' = min(C, 1024) channels; group g
+  // sums ranges g, g + G, ...; groups are folded in order.
+  for (int c0 = 0; c0 < C; c0 += 1024) {
+    const int cc = min(C - c0, 1024), G = 1024 / cc;
+    const int g = threadIdx.x / cc, c = threadIdx.x - g * cc;
+    if (g < G) {
+      float a = 0.f;
+      for (int b = g; b < kSePart; b += G) a += part[b * C + c0 + c];
+      red[g * cc + c] = a;
+    }
+    __syncthreads();
+    for (int k = threadIdx.x; k < cc; k += blockDim.x) {
+      float a = 0.f;
+      for (int q = 0; q < G; ++q) a += red[q * cc + k];
+      mean[c0 + k] = a * inv_n;
+    }
+    __syncthreads();
   }
-  __syncthreads();
   for (int r = threadIdx.x; r < R; r += blockDim.x) {  // fc.0: Linear(C, C/16, bias=False) + ReLU
     float a = 0.f;
     for (int c = 0; c < C; ++c) a += w1[r * C + c] * mean[c];
@@ -236,14 +322,27 @@ __global__ void channel_div_kernel(View x, const float *q, View y) {
   st<float>(y.p, pix * y.cs + y.co + c, ld<float>(x.p, pix * x.cs + x.co + c) / q[c]);
 }
 
-template <typename T>
+// y = a + x * s[c], V channels per thread (V = 1: scalar views)
+template <typename T, int V>
 __global__ void se_apply_kernel(View a, View x, const float *s, View y) {
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= (int64_t)y.H * y.W * y.C) return;
-  const int c = (int)(idx % y.C);
-  const int64_t pix = idx / y.C;
-  const float t = ld<T>(x.p, pix * x.cs + x.co + c) * s[c];
-  st<T>(y.p, pix * y.cs + y.co + c, ld<T>(a.p, pix * a.cs + a.co + c) + t);
+  const int CV = y.C / V;
+  if (idx >= (int64_t)y.H * y.W * CV) return;
+  const int c = (int)(idx % CV) * V;
+  const int64_t pix = idx / CV;
+  float u[V], w[V];
+  VecLd<T, V>::load(x.p, pix * x.cs + x.co + c, u);
+  VecLd<T, V>::load(a.p, pix * a.cs + a.co + c, w);
+#pragma unroll
+  for (int j = 0; j < V; ++j) w[j] += u[j] * s[c + j];
+  VecLd<T, V>::store(y.p, pix * y.cs + y.co + c, w);
+}
+
+// 16-byte vector access to V consecutive channels is legal for this view
+bool vec_ok(const dcvc_tensor &t, int V) {
+  const int es = t.dtype == DCVC_F32 ? 4 : 2;
+  return t.C % V == 0 && t.cstride % V == 0 && t.coff % V == 0 && (reinterpret_cast<uintptr_t>(t.ptr) % 16) == 0 &&
+         V * es == 16;
 }
 
 bool dp_ok(const dcvc_tensor &buf, const dcvc_tensor &sm, int k, int C) {
@@ -343,12 +442,19 @@ extern "C" int dcvc_se_scale(dcvc_tensor x, const float *w1, const float *w2, in
   if (!ok(x) || !w1 || !w2 || !work || !scale_out || reduced < 1 || reduced > 64 || x.C > 1024)
     return DCVC_HIP_EINVAL;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  if (x.dtype == DCVC_F32)
-    hipLaunchKernelGGL((se_partial_kernel<float>), dim3(kSePart), dim3(128), 0, st, mk(x), work);
-  else
-    hipLaunchKernelGGL((se_partial_kernel<uint16_t>), dim3(kSePart), dim3(128), 0, st, mk(x), work);
+  const int V = x.dtype == DCVC_F32 ? 4 : 8;
+  if (vec_ok(x, V) && x.C / V <= 256) {
+    if (x.dtype == DCVC_F32)
+      hipLaunchKernelGGL((se_partial_kernel<float, 4>), dim3(kSePart), dim3(256), 0, st, mk(x), work);
+    else
+      hipLaunchKernelGGL((se_partial_kernel<uint16_t, 8>), dim3(kSePart), dim3(256), 0, st, mk(x), work);
+  } else if (x.dtype == DCVC_F32) {
+    hipLaunchKernelGGL((se_partial_scalar_kernel<float>), dim3(kSePart), dim3(128), 0, st, mk(x), work);
+  } else {
+    hipLaunchKernelGGL((se_partial_scalar_kernel<uint16_t>), dim3(kSePart), dim3(128), 0, st, mk(x), work);
+  }
   DCVC_LAUNCH_CHECK();
-  hipLaunchKernelGGL(se_fc_kernel, dim3(1), dim3(256), 0, st, work, x.C, reduced,
+  hipLaunchKernelGGL(se_fc_kernel, dim3(1), dim3(1024), 0, st, work, x.C, reduced,
                      1.f / (float)((int64_t)x.H * x.W), w1, w2, scale_out);
   DCVC_LAUNCH_CHECK();
   return DCVC_HIP_OK;
@@ -359,11 +465,17 @@ extern "C" int dcvc_se_apply(dcvc_tensor a, dcvc_tensor x, const float *scale, d
       x.C != y.C || a.H != y.H || x.H != y.H || a.W != y.W || x.W != y.W)
     return DCVC_HIP_EINVAL;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  const unsigned g = blocks_for((int64_t)y.H * y.W * y.C);
-  if (y.dtype == DCVC_F32)
-    hipLaunchKernelGGL((se_apply_kernel<float>), dim3(g), dim3(256), 0, st, mk(a), mk(x), scale, mk(y));
-  else
-    hipLaunchKernelGGL((se_apply_kernel<uint16_t>), dim3(g), dim3(256), 0, st, mk(a), mk(x), scale, mk(y));
+  const int V = y.dtype == DCVC_F32 ? 4 : 8;
+  const bool vec = vec_ok(a, V) && vec_ok(x, V) && vec_ok(y, V);
+  const unsigned g = blocks_for((int64_t)y.H * y.W * y.C / (vec ? V : 1));
+#define LAUNCH(T, VV) \
+  hipLaunchKernelGGL((se_apply_kernel<T, VV>), dim3(g), dim3(256), 0, st, mk(a), mk(x), scale, mk(y))
+  if (y.dtype == DCVC_F32) {
+    if (vec) LAUNCH(float, 4); else LAUNCH(float, 1);
+  } else {
+    if (vec) LAUNCH(uint16_t, 8); else LAUNCH(uint16_t, 1);
+  }
+#undef LAUNCH
   DCVC_LAUNCH_CHECK();
   return DCVC_HIP_OK;
 }

@@ -131,14 +131,15 @@ __global__ void copy_kernel(View x, View y) {
 }
 
 template <typename TY>
-__global__ void frame_kernel(const uint8_t *src, int h, int w, View y) {
+__global__ void frame_kernel(const uint8_t *src, int h, int w, int zero_pad, View y) {
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= (int64_t)y.H * y.W * 3) return;
   const int c = (int)(idx % 3);
   const int64_t pix = idx / 3;
   const int py = (int)(pix / y.W), px = (int)(pix - (int64_t)py * y.W);
   const int sy = min(py, h - 1), sx = min(px, w - 1);
-  const float v = (float)src[((int64_t)c * h + sy) * w + sx] / 255.f;
+  float v = (float)src[((int64_t)c * h + sy) * w + sx] / 255.f;
+  if (zero_pad && (py >= h || px >= w)) v = 0.f;
   st<TY>(y.p, pix * y.cs + y.co + c, v);
 }
 
@@ -397,16 +398,24 @@ extern "C" int dcvc_pad_replicate(dcvc_tensor x, dcvc_tensor y, void *stream) {
   return copy_impl(x, y, stream);
 }
 
-extern "C" int dcvc_frame_to_nhwc(const uint8_t *src, int h, int w, dcvc_tensor y, void *stream) {
+static int frame_impl(const uint8_t *src, int h, int w, int zero_pad, dcvc_tensor y, void *stream) {
   if (!src || !ok(y) || y.C != 3 || h <= 0 || w <= 0 || y.H < h || y.W < w) return DCVC_HIP_EINVAL;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const unsigned g = blocks_for((int64_t)y.H * y.W * 3);
   if (y.dtype == DCVC_F32)
-    hipLaunchKernelGGL((frame_kernel<float>), dim3(g), dim3(256), 0, st, src, h, w, mk(y));
+    hipLaunchKernelGGL((frame_kernel<float>), dim3(g), dim3(256), 0, st, src, h, w, zero_pad, mk(y));
   else
-    hipLaunchKernelGGL((frame_kernel<uint16_t>), dim3(g), dim3(256), 0, st, src, h, w, mk(y));
+    hipLaunchKernelGGL((frame_kernel<uint16_t>), dim3(g), dim3(256), 0, st, src, h, w, zero_pad, mk(y));
   DCVC_LAUNCH_CHECK();
   return DCVC_HIP_OK;
+}
+
+extern "C" int dcvc_frame_to_nhwc(const uint8_t *src, int h, int w, dcvc_tensor y, void *stream) {
+  return frame_impl(src, h, w, 0, y, stream);
+}
+
+extern "C" int dcvc_frame_to_nhwc_zero_pad(const uint8_t *src, int h, int w, dcvc_tensor y, void *stream) {
+  return frame_impl(src, h, w, 1, y, stream);
 }
 
 extern "C" int dcvc_quadtree_encode_step(dcvc_tensor y, dcvc_tensor params, dcvc_tensor sm, int k,

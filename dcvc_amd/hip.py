@@ -64,6 +64,7 @@ HIP_SYMBOLS = [
     ("dcvc_copy", _i, [_T, _T, _vp]),
     ("dcvc_pad_replicate", _i, [_T, _T, _vp]),
     ("dcvc_frame_to_nhwc", _i, [_vp, _i, _i, _T, _vp]),
+    ("dcvc_frame_to_nhwc_zero_pad", _i, [_vp, _i, _i, _T, _vp]),
     ("dcvc_quadtree_encode_step", _i, [_T, _T, _T, _i, _T, _T, _vp, _vp, _f, _f, _vp]),
     ("dcvc_quadtree_indexes_step", _i, [_T, _T, _i, _vp, _f, _f, _vp]),
     ("dcvc_quadtree_decode_step", _i, [_T, _T, _i, _vp, _T, _T, _vp]),
@@ -356,8 +357,11 @@ def pad_replicate(x, y):
     return y
 
 
-def frame_to_nhwc(src_u8, h, w, y):
-    check(lib().dcvc_frame_to_nhwc(src_u8.data_ptr(), h, w, y.c(), stream()), "frame_to_nhwc")
+def frame_to_nhwc(src_u8, h, w, y, zero_pad=False):
+    if zero_pad:
+        check(lib().dcvc_frame_to_nhwc_zero_pad(src_u8.data_ptr(), h, w, y.c(), stream()), "frame_to_nhwc_zero_pad")
+    else:
+        check(lib().dcvc_frame_to_nhwc(src_u8.data_ptr(), h, w, y.c(), stream()), "frame_to_nhwc")
     return y
 
 

@@ -166,6 +166,10 @@ int dcvc_pad_replicate(dcvc_tensor x, dcvc_tensor y, void *stream);
 /* uint8 CHW frame -> float NHWC /255 with replicate padding to y's size. */
 int dcvc_frame_to_nhwc(const uint8_t *src, int h, int w, dcvc_tensor y,
                        void *stream);
+/* Same with zero padding: DCVC-HEM's harness pads frames with zeros to a
+ * multiple of 64 (DCVC-HEM/test_video.py:113-119, F.pad mode="constant"). */
+int dcvc_frame_to_nhwc_zero_pad(const uint8_t *src, int h, int w, dcvc_tensor y,
+                                void *stream);
 
 /*
  * Quadtree (four-part) prior step k, encoder side

@@ -209,6 +209,21 @@ def test_resize_and_pool():
     assert torch.equal(back(mp), F.max_pool2d(x, 2, 2))
 
 
+@pytest.mark.parametrize("zero_pad", [False, True])
+def test_frame_to_nhwc_padding(zero_pad):
+    """uint8 CHW frame -> float NHWC /255, padded to the harness's multiple:
+    replicate for DC (test_video.py:130), zeros for HEM (test_video.py:113-119)."""
+    h = K()
+    u8 = torch.randint(0, 256, (3, 37, 50), dtype=torch.uint8)
+    ref = u8.float().unsqueeze(0) / 255.0
+    ref = F.pad(ref, (0, 14, 0, 27), mode="constant", value=0) if zero_pad else F.pad(ref, (0, 14, 0, 27),
+                                                                                    mode="replicate")
+    y = h.empty(64, 64, 3, h.F32, torch.device("cuda"))
+    h.frame_to_nhwc(u8.cuda(), 37, 50, y, zero_pad=zero_pad)
+    torch.cuda.synchronize()
+    assert torch.equal(back(y), ref)
+
+
 def test_offset_diversity_matches_oracle():
     from oracle import dc_oracle as O
     h = K()
@@ -487,3 +502,36 @@ def test_persistent_depthconv_block_equals_per_tile_kernel(shape):
     torch.cuda.synchronize()
     assert names[0].startswith("dcbp_kernel") and names[1].startswith("dcb_kernel"), names
     assert torch.equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("dt,C,view", [("f32", 64, False), ("bf16", 64, False), ("bf16", 256, False),
+                                       ("bf16", 48, True), ("f32", 36, False)])
+def test_se_layer_matches_torch(dt, C, view):
+    """SELayer (DCVC-HEM/src/models/video_net.py:157-170) + the residual
+    apply of ConvBlockResidual (:173-188): vector and scalar-view paths."""
+    h = K()
+    dtype = h.F32 if dt == "f32" else h.BF16
+    R = max(1, C // 16)
+    x = torch.randn(1, C, 45, 77)
+    a = torch.randn(1, C, 45, 77)
+    w1 = torch.randn(R, C) * 0.3
+    w2 = torch.randn(C, R) * 0.3
+    if view:   # channel view at offset 3 of a wider buffer: scalar path
+        big = torch.randn(1, C + 16, 45, 77)
+        big[:, 3:3 + C] = x
+        xa = to_act(big, dtype).ch(3, C)
+    else:
+        xa = to_act(x, dtype)
+    x = back(xa)
+    aa = to_act(a, dtype)
+    a = back(aa)
+    work = torch.empty(256 * C, dtype=torch.float32, device="cuda")
+    s = torch.empty(C, dtype=torch.float32, device="cuda")
+    h.se_scale(xa, w1.cuda(), w2.cuda(), work, s)
+    y = h.se_apply(aa, xa, s)
+    torch.cuda.synchronize()
+    ref_s = torch.sigmoid(w2 @ torch.relu(w1 @ x.mean((-1, -2))[0]))
+    assert (s.cpu() - ref_s).abs().max().item() < 1e-5
+    ref_y = a + x * ref_s[None, :, None, None]
+    tol = 1e-5 if dt == "f32" else 1e-2
+    assert rel_err(back(y), ref_y) < tol
