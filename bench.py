@@ -40,8 +40,10 @@ def parse():
                     help="HEM rate point: index into the checkpoint's q_scale ladders (test_video.py:274-300)")
     ap.add_argument("--steps", type=int, default=32)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--height", type=int, default=1080)
-    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=None, help="default 1080 (2160 with --yuv420)")
+    ap.add_argument("--width", type=int, default=None, help="default 1920 (3840 with --yuv420)")
+    ap.add_argument("--yuv420", action="store_true",
+                    help="config C4: DCVC-DC YUV420 source coded as YCbCr 4:4:4 (dist_in_yuv420), 3840x2160")
     ap.add_argument("--gop", type=int, default=32)
     ap.add_argument("--q_index", type=int, default=0)
     ap.add_argument("--precision", choices=["fast", "parity"], default="fast")
@@ -50,7 +52,14 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--profile-out", default="", help="per-shape kernel timing JSON of one P-frame")
-    return ap.parse_args()
+    a = ap.parse_args()
+    if a.yuv420 and a.model != "dc":
+        ap.error("--yuv420 is the DCVC-DC YUV path (config C4)")
+    if a.height is None:
+        a.height = 2160 if a.yuv420 else 1080
+    if a.width is None:
+        a.width = 3840 if a.yuv420 else 1920
+    return a
 
 
 HEM_GAIN = 1.6   # tests/golden/make_golden_hem.py: latents beyond 0/+-1 without blow-up
@@ -143,12 +152,13 @@ def cpu_baseline(isd, psd, args):
         dec = code(pnet.compress(frames[1], dpb, False, args.q_index, 1), "p_")
         pnet.decompress(dpb, dec, h, w, False, args.q_index, 1)
         t_p = time.time() - t0
-    area = (1088 * 1920) / (h * w)
+    Hp, Wp = (args.height + 15) // 16 * 16, (args.width + 15) // 16 * 16
+    area = (Hp * Wp) / (h * w)
     gop = args.gop
     fps = gop / (area * (t_i + (gop - 1) * t_p))
     return {"value": fps, "unit": "frames/s", "cores": threads, "kind": "port",
             "sample": f"oracle write-mode I+P encode+decode at {h}x{w} (I {t_i:.1f}s, P {t_p:.1f}s), "
-                      f"scaled x{area:.1f} by area to 1088x1920, GOP {gop} average"}
+                      f"scaled x{area:.1f} by area to {Hp}x{Wp}, GOP {gop} average"}
 
 
 def hem_q(sd_i, sd_p, rate):
@@ -192,20 +202,33 @@ def cpu_baseline_hem(isd, psd, args):
         t0 = time.time()
         pnet.decompress(dpb, coder(pnet.compress(frames[1], dpb, qmv, qy)), h, w, qmv, qy)
         t_p = time.time() - t0
-    area = (1088 * 1920) / (h * w)
+    Hp, Wp = (args.height + 63) // 64 * 64, (args.width + 63) // 64 * 64
+    area = (Hp * Wp) / (h * w)
     gop = args.gop
     fps = gop / (area * (t_i + (gop - 1) * t_p))
     return {"value": fps, "unit": "frames/s", "cores": threads, "kind": "port",
             "sample": f"HEM oracle write-mode I+P encode+decode at {h}x{w} (I {t_i:.1f}s, P {t_p:.1f}s), "
-                      f"scaled x{area:.2f} by area to 1088x1920, GOP {gop} average"}
+                      f"scaled x{area:.2f} by area to {Hp}x{Wp}, GOP {gop} average"}
 
 
-def pmc_traffic(kname):
-    """HBM bytes per launch of `kname` (instantiation@grid, which fixes the
-    launch geometry) from the committed rocprofv3 PMC summary
-    (profiles/*_pmc.json, written by scripts/pmc_summary.py from separate
-    FETCH_SIZE / WRITE_SIZE passes, FETCH_SIZE doubled per the gfx950
-    calibration); None when no summary has this kernel."""
+def workload_key(argv):
+    """(model, yuv420, height, width) of a bench.py command line."""
+    toks = argv.split() if isinstance(argv, str) else list(argv)
+
+    def opt(name, default):
+        return toks[toks.index(name) + 1] if name in toks else default
+    yuv = "--yuv420" in toks
+    return (opt("--model", "dc"), yuv, int(opt("--height", 2160 if yuv else 1080)),
+            int(opt("--width", 3840 if yuv else 1920)))
+
+
+def pmc_traffic(kname, workload):
+    """HBM bytes per launch of `kname` (instantiation@grid) from the committed
+    rocprofv3 PMC summary (profiles/*_pmc.json, written by
+    scripts/pmc_summary.py from separate FETCH_SIZE / WRITE_SIZE passes,
+    FETCH_SIZE doubled per the gfx950 calibration) of the same workload
+    (model, source format, frame size); None when no summary has this kernel
+    on this workload."""
     import glob
     for path in sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)),
                                               "profiles", "*_pmc.json")), reverse=True):
@@ -213,6 +236,8 @@ def pmc_traffic(kname):
             with open(path) as f:
                 d = json.load(f)
         except (OSError, ValueError):
+            continue
+        if workload_key(d.get("command", "")) != workload:
             continue
         for e in d.get("kernels", []):
             if e.get("kernel") == kname and e.get("hbm_bytes_per_launch"):
@@ -236,7 +261,8 @@ def main():
 
     from dcvc_amd import hip as K
     from dcvc_amd.layers import Precision
-    from dcvc_amd.synth import moving_pattern
+    from dcvc_amd.harness import FrameStage, psnr_rgb, psnr_yuv
+    from dcvc_amd.synth import moving_pattern, moving_pattern_yuv420
 
     hem = args.model == "hem"
     isd, psd = make_weights(dist, rank, device, args.model)
@@ -255,19 +281,26 @@ def main():
 
     h, w = args.height, args.width
     align = 64 if hem else 16     # HEM test_video.py:113-119 pads to 64, DC to 16
-    H, W = (h + align - 1) // align * align, (w + align - 1) // align * align
     nframes = args.warmup + args.steps
-    frames = [torch.from_numpy(moving_pattern(h, w, t, seed=shard_seed(rank))).to(device) for t in range(nframes)]
+    # run_test's frame handling (dcvc_amd.harness.FrameStage): uint8 source
+    # resident in HBM, converted to the padded NHWC input inside the step;
+    # the distortion (in-place clamp + squared-error sums) is part of the step
+    stage = FrameStage(h, w, align, args.yuv420, zero_pad=hem, frame_num=nframes + 2, device=device)
+    H, W = stage.H, stage.W
+    if args.yuv420:
+        frames = [tuple(torch.from_numpy(a).to(device) for a in moving_pattern_yuv420(h, w, t, seed=shard_seed(rank)))
+                  for t in range(nframes)]
+    else:
+        frames = [torch.from_numpy(moving_pattern(h, w, t, seed=shard_seed(rank))).to(device) for t in range(nframes)]
     out_dir = f"/dev/shm/dcvc_bench_{os.getpid()}"
     os.makedirs(out_dir, exist_ok=True)
-    x = K.empty(H, W, 3, K.F32, device)
     state = {"dpb": None}
     bits = []
     kinds = []
 
     def step(i):
-        # uint8 CHW -> padded NHWC: replicate (DC test_video.py:130) / zeros (HEM)
-        K.frame_to_nhwc(frames[i], h, w, x, zero_pad=hem)
+        # uint8 source -> padded NHWC: replicate (DC test_video.py:130) / zeros (HEM)
+        x = stage.load(frames[i])
         path = os.path.join(out_dir, f"{i}.bin")
         if hem:
             if i % args.gop == 0:
@@ -290,6 +323,7 @@ def main():
             state["dpb"] = r["dpb"]
             kinds.append("P")
         bits.append(r["bit"])
+        stage.distortion(state["dpb"]["ref_frame"], frames[i], i)
 
     for i in range(args.warmup):
         step(i)
@@ -344,7 +378,7 @@ def main():
             roof = {"bound": "hbm", "achieved": round(ach, 2), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                     "frac": round(ach / PEAK_HBM_GBS, 5)}
         kname, _, shape = key.partition(" | ")
-        tr = pmc_traffic(kname)
+        tr = pmc_traffic(kname, (args.model, args.yuv420, h, w))
         roof["traffic"] = tr["hbm_bytes_per_launch"] if tr else None
         if tr:
             roof["traffic_source"] = tr["source"]
@@ -371,8 +405,15 @@ def main():
         if not args.no_cpu_baseline and world == 1:
             cpu = cpu_baseline_hem(isd, psd, args) if hem else cpu_baseline(isd, psd, args)
         timed_bits = bits[args.warmup:nframes]
+        sse = stage.sums()[args.warmup:nframes]
+        if args.yuv420:
+            per = [psnr_yuv(e, h, w) for e in sse]
+            psnr = {"psnr": round(float(np.mean([p[3] for p in per])), 4),
+                    "psnr_yuv": [round(float(np.mean([p[c] for p in per])), 4) for c in range(3)]}
+        else:
+            psnr = {"psnr": round(float(np.mean([psnr_rgb(e, h, w) for e in sse])), 4)}
         line = {
-            "metric": f"encode+decode fps @1080p per GPU ({'DCVC-HEM' if hem else 'DCVC-DC'} write mode, "
+            "metric": f"encode+decode fps @{h}p per GPU ({'DCVC-HEM' if hem else 'DCVC-DC'} write mode, "
                       "real bitstreams)",
             "value": round(world * args.steps / elapsed, 4),
             "unit": "frames/s",
@@ -386,14 +427,16 @@ def main():
             "dtype": "bf16" if args.precision == "fast" else "f32",
             "data": "synthetic (moving sinusoid + noise frames, seeded random weights)",
             "config": {"workload": (f"C2 DCVC-HEM RGB {w}x{h} (zero pad {W}x{H}) IP={args.gop} write mode"
-                                    if hem else f"C3 DCVC-DC RGB {w}x{h} (pad {W}x{H}) IP={args.gop} write mode"),
+                                    if hem else
+                                    f"C4 DCVC-DC YUV420 {w}x{h} (pad {W}x{H}) IP={args.gop} write mode" if args.yuv420
+                                    else f"C3 DCVC-DC RGB {w}x{h} (pad {W}x{H}) IP={args.gop} write mode"),
                        "gop": args.gop, "precision": args.precision,
                        **({"rate": args.rate, "q_scales": [round(qi, 4), round(qmv, 4), round(qy, 4)]} if hem
                           else {"q_index": args.q_index, "stream_part": args.stream_part}), "parallelism": f"sequence-sharded x{world}",
                        "I_frames_timed": n_i,
                        "ms_I": round(1e3 * float(np.mean(ti)), 2) if ti else None,
                        "ms_P": round(1e3 * float(np.mean(tp)), 2) if tp else None,
-                       "bpp": round(float(np.mean(timed_bits)) / (h * w), 5)},
+                       "bpp": round(float(np.mean(timed_bits)) / (h * w), 5), **psnr},
             "roofline": roof,
             "cpu_baseline": cpu,
         }

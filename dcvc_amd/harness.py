@@ -1,0 +1,398 @@
+"""The test harness around the codecs: ``run_test`` of DCVC-DC/test_video.py:
+71-237 (RGB and YUV420 sources, I/P schedule, DPB aliasing, in-place clamp,
+crop, PSNR, the JSON log of src/utils/common.py:44-140) and of
+DCVC-HEM/test_video.py:80-172, with the per-frame tensor work on the GPU.
+
+Source frames cross to the GPU as uint8 (a quarter of the reference's fp32
+upload).  ``FrameStage`` turns them into the padded NHWC codec input
+(``dcvc_frame_to_nhwc`` / ``dcvc_yuv420_to_nhwc``) and computes each frame's
+distortion with ``dcvc_frame_sse``, which also performs
+``recon_frame.clamp_(0, 1)`` on the DPB frame in place.  The squared-error
+sums stay on the device until the end of the sequence (one transfer), and the
+PSNR formulas are evaluated on the host exactly as the reference writes them.
+
+MS-SSIM (``calc_ssim``; DCVC-HEM always computes it) needs the
+``pytorch_msssim`` package for RGB, which is absent from this image; it is
+reported as 0 with ``msssim_unavailable`` set in the log.
+"""
+import os
+import time
+
+import numpy as np
+import torch
+
+from . import hip as K
+from .stream_helper import get_padding_size
+
+
+# ----------------------------------------------------------------- readers
+class YUVReader:
+    """Raw 8-bit YUV420 file reader (DCVC-DC/src/utils/video_reader.py:
+    121-161).  ``read_one_frame`` returns uint8 ``(y (h, w), uv (2, h/2,
+    w/2))``, or ``(None, None)`` at the end of the file; the reference's
+    float conversion (x / 255) happens on the GPU."""
+
+    def __init__(self, src_path, width, height, src_format="420", skip_frame=0):
+        if src_format != "420":
+            raise ValueError("only 420 sources are supported (video_reader.py:127)")
+        if not src_path.endswith(".yuv"):
+            src_path = src_path + ".yuv"
+        self.src_path, self.width, self.height = src_path, width, height
+        self.y_size = width * height
+        self.uv_size = width * height // 2
+        self.eof = False
+        self.file = open(src_path, "rb")  # noqa: SIM115 (closed in close())
+        for _ in range(skip_frame):
+            if not self._read():
+                break
+
+    def _read(self):
+        y = self.file.read(self.y_size)
+        uv = self.file.read(self.uv_size)
+        if len(y) < self.y_size or len(uv) < self.uv_size:
+            self.eof = True
+            return None
+        return y, uv
+
+    def read_one_frame(self, dst_format="420"):
+        if dst_format != "420":
+            raise ValueError("YUVReader hands over 420 planes; RGB sources use PNGReader")
+        if self.eof:
+            return None, None
+        r = self._read()
+        if r is None:
+            return None, None
+        y = np.frombuffer(r[0], dtype=np.uint8).reshape(self.height, self.width)
+        uv = np.frombuffer(r[1], dtype=np.uint8).reshape(2, self.height // 2, self.width // 2)
+        return y, uv
+
+    def close(self):
+        self.file.close()
+
+
+class PNGReader:
+    """Folder of im1.png / im00001.png frames (video_reader.py:44-80);
+    returns uint8 CHW RGB, or None at the end."""
+
+    def __init__(self, src_path, width, height, start_num=1):
+        pngs = os.listdir(src_path)
+        if "im1.png" in pngs:
+            self.padding = 1
+        elif "im00001.png" in pngs:
+            self.padding = 5
+        else:
+            raise ValueError("unknown image naming convention; please specify")
+        self.src_path, self.width, self.height = src_path, width, height
+        self.current_frame_index = start_num
+        self.eof = False
+
+    def read_one_frame(self, dst_format="rgb"):
+        from PIL import Image
+        if dst_format != "rgb":
+            raise ValueError("PNGReader hands over RGB frames")
+        if self.eof:
+            return None
+        p = os.path.join(self.src_path, f"im{str(self.current_frame_index).zfill(self.padding)}.png")
+        if not os.path.exists(p):
+            self.eof = True
+            return None
+        rgb = np.asarray(Image.open(p).convert("RGB")).transpose(2, 0, 1)
+        if rgb.shape[1:] != (self.height, self.width):
+            raise ValueError(f"{p}: {rgb.shape[1:]} != {(self.height, self.width)}")
+        self.current_frame_index += 1
+        return np.ascontiguousarray(rgb)
+
+    def close(self):
+        self.current_frame_index = 1
+
+
+class ArrayReader:
+    """In-memory frames (synthetic sequences, tests): uint8 CHW RGB arrays,
+    or (y, uv) uint8 plane pairs for YUV420."""
+
+    def __init__(self, frames):
+        self.frames = list(frames)
+        self.i = 0
+
+    def read_one_frame(self, dst_format="rgb"):
+        if self.i >= len(self.frames):
+            return (None, None) if dst_format == "420" else None
+        f = self.frames[self.i]
+        self.i += 1
+        return f
+
+    def close(self):
+        pass
+
+
+# ----------------------------------------------------------- device staging
+class FrameStage:
+    """Device side of one sequence: uint8 source upload, padded NHWC codec
+    input, and the per-frame squared-error sums (frame_num x 3, fp64)."""
+
+    def __init__(self, h, w, align, yuv420, zero_pad, frame_num, device):
+        self.h, self.w, self.yuv, self.zero_pad = h, w, yuv420, zero_pad
+        _, pr, _, pb = get_padding_size(h, w, align)
+        self.H, self.W = h + pb, w + pr
+        self.dev = device
+        self.x = K.empty(self.H, self.W, 3, K.F32, device)
+        self.ws = K.frame_sse_workspace(device)
+        self.sse = torch.zeros((max(frame_num, 1), 3), dtype=torch.float64, device=device)
+
+    def upload(self, frame):
+        """Host uint8 frame (CHW RGB, or (y, uv)) -> device tensors."""
+        if self.yuv:
+            y, uv = frame
+            return (torch.from_numpy(np.ascontiguousarray(y)).to(self.dev, non_blocking=True),
+                    torch.from_numpy(np.ascontiguousarray(uv)).to(self.dev, non_blocking=True))
+        return torch.from_numpy(np.ascontiguousarray(frame)).to(self.dev, non_blocking=True)
+
+    def load(self, dframe):
+        """Device uint8 frame -> padded NHWC fp32 codec input (test_video.py:
+        108-132: ycbcr420_to_444(order=0) for YUV, x / 255, F.pad)."""
+        if self.yuv:
+            K.yuv420_to_nhwc(dframe[0], dframe[1], self.h, self.w, self.x)
+        else:
+            K.frame_to_nhwc(dframe, self.h, self.w, self.x, zero_pad=self.zero_pad)
+        return self.x
+
+    def distortion(self, recon, dframe, slot):
+        """recon_frame.clamp_(0, 1), crop, and the squared-error sums of the
+        frame into row ``slot`` (test_video.py:169-195)."""
+        from .dc.video_model import as_act
+        r = as_act(recon)
+        if self.yuv:
+            K.frame_sse(r, dframe[0], self.h, self.w, self.ws, self.sse[slot], uv_u8=dframe[1])
+        else:
+            K.frame_sse(r, dframe, self.h, self.w, self.ws, self.sse[slot])
+
+    def sums(self):
+        return self.sse.cpu().numpy()
+
+
+def psnr_rgb(sse3, h, w):
+    """PSNR() of test_video.py:65-68: mse = mean((x_hat - x)^2) as an fp32
+    tensor, psnr = 20 * log10(1 / sqrt(mse)) in fp32."""
+    mse = torch.tensor(float(np.sum(sse3)) / (3.0 * h * w), dtype=torch.float32)
+    return (20 * torch.log10(1 / torch.sqrt(mse))).item()
+
+
+def calc_psnr_from_sse(sse, n, data_range=1.0):
+    """calc_psnr (src/utils/metrics.py:81-92) from an fp64 squared-error sum."""
+    mse = sse / n
+    if mse > 1e-10:
+        return 10 * np.log10(data_range * data_range / mse)
+    return 999.9
+
+
+def psnr_yuv(sse3, h, w):
+    """(psnr_y, psnr_u, psnr_v, (6 y + u + v) / 8), test_video.py:177-181."""
+    py = calc_psnr_from_sse(sse3[0], h * w)
+    pu = calc_psnr_from_sse(sse3[1], (h // 2) * (w // 2))
+    pv = calc_psnr_from_sse(sse3[2], (h // 2) * (w // 2))
+    return py, pu, pv, (6 * py + pu + pv) / 8
+
+
+# ---------------------------------------------------------------- run_test
+def generate_log_json(frame_num, frame_pixel_num, test_time, frame_types, bits, psnrs, ssims,
+                      psnrs_y=None, psnrs_u=None, psnrs_v=None, ssims_y=None, ssims_u=None, ssims_v=None,
+                      verbose=False):
+    """DCVC-DC/src/utils/common.py:44-140 (same keys and averages)."""
+    yuv = psnrs_y is not None
+    acc = {k: {"bits": 0, "psnr": 0, "ssim": 0, "y": 0, "u": 0, "v": 0, "sy": 0, "su": 0, "sv": 0, "n": 0}
+           for k in (0, 1)}
+    for i in range(frame_num):
+        a = acc[0 if frame_types[i] == 0 else 1]
+        a["bits"] += bits[i]
+        a["psnr"] += psnrs[i]
+        a["ssim"] += ssims[i]
+        a["n"] += 1
+        if yuv:
+            for key, src in (("y", psnrs_y), ("u", psnrs_u), ("v", psnrs_v),
+                             ("sy", ssims_y), ("su", ssims_u), ("sv", ssims_v)):
+                a[key] += src[i]
+    ai, ap = acc[0], acc[1]
+    log = {"frame_pixel_num": frame_pixel_num, "i_frame_num": ai["n"], "p_frame_num": ap["n"],
+           "ave_i_frame_bpp": ai["bits"] / ai["n"] / frame_pixel_num,
+           "ave_i_frame_psnr": ai["psnr"] / ai["n"], "ave_i_frame_msssim": ai["ssim"] / ai["n"]}
+    if yuv:
+        for c in "yuv":
+            log[f"ave_i_frame_psnr_{c}"] = ai[c] / ai["n"]
+        for c in "yuv":
+            log[f"ave_i_frame_msssim_{c}"] = ai["s" + c] / ai["n"]
+    if verbose:
+        log["frame_bpp"] = list(np.array(bits) / frame_pixel_num)
+        log["frame_psnr"] = psnrs
+        log["frame_msssim"] = ssims
+        log["frame_type"] = frame_types
+        if yuv:
+            log.update(frame_psnr_y=psnrs_y, frame_psnr_u=psnrs_u, frame_psnr_v=psnrs_v,
+                       frame_msssim_y=ssims_y, frame_msssim_u=ssims_u, frame_msssim_v=ssims_v)
+    log["test_time"] = test_time
+    if ap["n"] > 0:
+        log["ave_p_frame_bpp"] = ap["bits"] / (ap["n"] * frame_pixel_num)
+        log["ave_p_frame_psnr"] = ap["psnr"] / ap["n"]
+        log["ave_p_frame_msssim"] = ap["ssim"] / ap["n"]
+        if yuv:
+            for c in "yuv":
+                log[f"ave_p_frame_psnr_{c}"] = ap[c] / ap["n"]
+            for c in "yuv":
+                log[f"ave_p_frame_msssim_{c}"] = ap["s" + c] / ap["n"]
+    else:
+        log["ave_p_frame_bpp"] = 0
+        log["ave_p_frame_psnr"] = 0
+        log["ave_p_frame_msssim"] = 0
+        if yuv:
+            for c in "yuv":
+                log[f"ave_p_frame_psnr_{c}"] = 0
+            for c in "yuv":
+                log[f"ave_p_frame_msssim_{c}"] = 0
+    log["ave_all_frame_bpp"] = (ai["bits"] + ap["bits"]) / (frame_num * frame_pixel_num)
+    log["ave_all_frame_psnr"] = (ai["psnr"] + ap["psnr"]) / frame_num
+    log["ave_all_frame_msssim"] = (ai["ssim"] + ap["ssim"]) / frame_num
+    if yuv:
+        for c in "yuv":
+            log[f"ave_all_frame_psnr_{c}"] = (ai[c] + ap[c]) / frame_num
+        for c in "yuv":
+            log[f"ave_all_frame_msssim_{c}"] = (ai["s" + c] + ap["s" + c]) / frame_num
+    return log
+
+
+def _reader(args, yuv):
+    if "src_reader" in args:
+        return args["src_reader"]
+    if args["src_type"] == "yuv420":
+        return YUVReader(args["src_path"], args["src_width"], args["src_height"])
+    if args["src_type"] == "png":
+        return PNGReader(args.get("src_path", args.get("img_path")), args["src_width"], args["src_height"])
+    raise ValueError(f"unknown src_type {args['src_type']!r}")
+
+
+def run_test(p_frame_net, i_frame_net, args):
+    """DCVC-DC/test_video.py:71-237 on the GPU codecs.  ``args`` takes the
+    reference's keys (frame_num, gop_size, write_stream, bin_folder,
+    src_type 'png' | 'yuv420', src_path, src_width, src_height,
+    dist_in_yuv420, q_in_ckpt, i_frame_q_index, verbose, calc_ssim) plus an
+    optional ``src_reader`` (an ArrayReader) in place of a file source.
+    YUV420 sources are coded as YCbCr 4:4:4 (``dist_in_yuv420``), as the
+    reference's yuv420 checkpoints expect."""
+    frame_num, gop_size = args["frame_num"], args["gop_size"]
+    write_stream = bool(args.get("write_stream", False))
+    verbose = args.get("verbose", 0)
+    if args.get("save_decoded_frame"):
+        raise NotImplementedError("save_decoded_frame: the video writers are out of scope (DESIGN.md §10)")
+    yuv = bool(args.get("dist_in_yuv420", False))
+    if yuv and args.get("src_type", "yuv420") != "yuv420" and "src_reader" not in args:
+        raise ValueError("dist_in_yuv420 needs a yuv420 source")
+    device = i_frame_net.dev
+    reader = _reader(args, yuv)
+    h, w = args["src_height"], args["src_width"]
+    stage = FrameStage(h, w, 16, yuv, zero_pad=False, frame_num=frame_num, device=device)
+    frame_types, bits = [], []
+    start_time = time.time()
+    p_frame_number = 0
+    enc_t = dec_t = 0.0
+    dpb = None
+    with torch.no_grad():
+        for frame_idx in range(frame_num):
+            frame = reader.read_one_frame(dst_format="420" if yuv else "rgb")
+            if frame is None or (yuv and frame[0] is None):
+                raise ValueError(f"source ended at frame {frame_idx} of {frame_num}")
+            dframe = stage.upload(frame)
+            x = stage.load(dframe)
+            bin_path = os.path.join(args["bin_folder"], f"{frame_idx}.bin") if write_stream else None
+            if frame_idx % gop_size == 0:
+                result = i_frame_net.encode_decode(x, args["q_in_ckpt"], args["i_frame_q_index"], bin_path,
+                                                   pic_height=h, pic_width=w)
+                dpb = {"ref_frame": result["x_hat"], "ref_feature": None, "ref_mv_feature": None,
+                       "ref_y": None, "ref_mv_y": None}
+                recon = result["x_hat"]
+                frame_types.append(0)
+            else:
+                # test_video.py:152-155 passes i_frame_q_index to the P codec too
+                result = p_frame_net.encode_decode(x, dpb, args["q_in_ckpt"], args["i_frame_q_index"], bin_path,
+                                                   pic_height=h, pic_width=w, frame_idx=frame_idx % 4)
+                dpb = result["dpb"]
+                recon = dpb["ref_frame"]
+                frame_types.append(1)
+                p_frame_number += 1
+                enc_t += result["encoding_time"]
+                dec_t += result["decoding_time"]
+            bits.append(result["bit"])
+            stage.distortion(recon, dframe, frame_idx)
+            if verbose >= 2:
+                print(f"frame {frame_idx}, bits: {bits[-1]:.3f}", flush=True)
+    sse = stage.sums()
+    test_time = time.time() - start_time
+    if verbose >= 1 and p_frame_number > 0:
+        print(f"encoding/decoding {p_frame_number} P frames, "
+              f"average encoding time {enc_t / p_frame_number * 1000:.0f} ms, "
+              f"average decoding time {dec_t / p_frame_number * 1000:.0f} ms.")
+    zeros = [0.0] * frame_num
+    if yuv:
+        per = [psnr_yuv(sse[i], h, w) for i in range(frame_num)]
+        log = generate_log_json(frame_num, h * w, test_time, frame_types, bits, [p[3] for p in per], zeros,
+                                [p[0] for p in per], [p[1] for p in per], [p[2] for p in per],
+                                zeros, zeros, zeros, verbose=verbose >= 1)
+    else:
+        psnrs = [psnr_rgb(sse[i], h, w) for i in range(frame_num)]
+        log = generate_log_json(frame_num, h * w, test_time, frame_types, bits, psnrs, zeros,
+                                verbose=verbose >= 1)
+    if args.get("calc_ssim"):
+        log["msssim_unavailable"] = True
+    return log
+
+
+def generate_log_json_hem(frame_num, frame_types, bits, psnrs, ssims, frame_pixel_num, test_time):
+    """DCVC-HEM/src/utils/common.py:63-104."""
+    log = generate_log_json(frame_num, frame_pixel_num, test_time, frame_types, bits, psnrs, ssims, verbose=True)
+    keep = ("frame_pixel_num", "i_frame_num", "p_frame_num", "ave_i_frame_bpp", "ave_i_frame_psnr",
+            "ave_i_frame_msssim", "frame_bpp", "frame_psnr", "frame_msssim", "frame_type", "test_time",
+            "ave_p_frame_bpp", "ave_p_frame_psnr", "ave_p_frame_msssim", "ave_all_frame_bpp",
+            "ave_all_frame_psnr", "ave_all_frame_msssim")
+    return {k: log[k] for k in keep if k in log}
+
+
+def run_test_hem(video_net, i_frame_net, args, device=None):
+    """DCVC-HEM/test_video.py:80-172: PNG (or in-memory) RGB source, zero
+    padding to a multiple of 64, q scales from ``args`` (i_frame_q_scale,
+    p_frame_mv_y_q_scale, p_frame_y_q_scale)."""
+    frame_num, gop_size = args["frame_num"], args["gop_size"]
+    write_stream = bool(args.get("write_stream", False))
+    if args.get("save_decoded_frame"):
+        raise NotImplementedError("save_decoded_frame: the PNG writer is out of scope (DESIGN.md §10)")
+    device = device if device is not None else i_frame_net.dev
+    reader = _reader({**args, "src_type": args.get("src_type", "png")}, False)
+    h, w = args["src_height"], args["src_width"]
+    stage = FrameStage(h, w, 64, False, zero_pad=True, frame_num=frame_num, device=device)
+    frame_types, bits = [], []
+    start_time = time.time()
+    dpb = None
+    with torch.no_grad():
+        for frame_idx in range(frame_num):
+            frame = reader.read_one_frame(dst_format="rgb")
+            if frame is None:
+                raise ValueError(f"source ended at frame {frame_idx} of {frame_num}")
+            dframe = stage.upload(frame)
+            x = stage.load(dframe)
+            bin_path = os.path.join(args["bin_folder"], f"{frame_idx}.bin") if write_stream else None
+            if frame_idx % gop_size == 0:
+                result = i_frame_net.encode_decode(x, args["i_frame_q_scale"], bin_path, pic_height=h, pic_width=w)
+                dpb = {"ref_frame": result["x_hat"], "ref_feature": None, "ref_y": None, "ref_mv_y": None}
+                recon = result["x_hat"]
+                frame_types.append(0)
+            else:
+                result = video_net.encode_decode(x, dpb, bin_path, pic_height=h, pic_width=w,
+                                                 mv_y_q_scale=args["p_frame_mv_y_q_scale"],
+                                                 y_q_scale=args["p_frame_y_q_scale"])
+                dpb = result["dpb"]
+                recon = dpb["ref_frame"]
+                frame_types.append(1)
+            bits.append(result["bit"])
+            stage.distortion(recon, dframe, frame_idx)
+    sse = stage.sums()
+    psnrs = [psnr_rgb(sse[i], h, w) for i in range(frame_num)]
+    log = generate_log_json_hem(frame_num, frame_types, bits, psnrs, [0.0] * frame_num, h * w,
+                                time.time() - start_time)
+    log["msssim_unavailable"] = True
+    return log

@@ -65,6 +65,9 @@ HIP_SYMBOLS = [
     ("dcvc_pad_replicate", _i, [_T, _T, _vp]),
     ("dcvc_frame_to_nhwc", _i, [_vp, _i, _i, _T, _vp]),
     ("dcvc_frame_to_nhwc_zero_pad", _i, [_vp, _i, _i, _T, _vp]),
+    ("dcvc_yuv420_to_nhwc", _i, [_vp, _vp, _i, _i, _T, _vp]),
+    ("dcvc_frame_sse_workspace", ctypes.c_int64, []),
+    ("dcvc_frame_sse", _i, [_T, _vp, _vp, _i, _i, _i, _vp, _vp, _vp]),
     ("dcvc_quadtree_encode_step", _i, [_T, _T, _T, _i, _T, _T, _vp, _vp, _f, _f, _vp]),
     ("dcvc_quadtree_indexes_step", _i, [_T, _T, _i, _vp, _f, _f, _vp]),
     ("dcvc_quadtree_decode_step", _i, [_T, _T, _i, _vp, _T, _T, _vp]),
@@ -363,6 +366,31 @@ def frame_to_nhwc(src_u8, h, w, y, zero_pad=False):
     else:
         check(lib().dcvc_frame_to_nhwc(src_u8.data_ptr(), h, w, y.c(), stream()), "frame_to_nhwc")
     return y
+
+
+def yuv420_to_nhwc(y_u8, uv_u8, h, w, out):
+    """uint8 device planes Y (h*w) and U|V (2*(h/2)*(w/2)) -> padded NHWC
+    YCbCr 4:4:4 fp32 (ycbcr420_to_444(order=0) + pad, test_video.py:111-132)."""
+    assert y_u8.dtype == torch.uint8 and uv_u8.dtype == torch.uint8
+    assert y_u8.numel() == h * w and uv_u8.numel() == 2 * (h // 2) * (w // 2)
+    check(lib().dcvc_yuv420_to_nhwc(y_u8.data_ptr(), uv_u8.data_ptr(), h, w, out.c(), stream()), "yuv420_to_nhwc")
+    return out
+
+
+def frame_sse_workspace(device):
+    n = int(lib().dcvc_frame_sse_workspace())
+    return torch.empty(n // 8, dtype=torch.float64, device=device)
+
+
+def frame_sse(x_hat, src_u8, h, w, workspace, out3, uv_u8=None):
+    """Clamp x_hat in place and write the 3 per-plane squared-error sums of
+    the h x w crop into out3 (fp64 device); see dcvc_frame_sse."""
+    assert x_hat.dtype == F32 and x_hat.C == 3 and out3.dtype == torch.float64 and out3.numel() >= 3
+    yuv = uv_u8 is not None
+    assert src_u8.numel() == (h * w if yuv else 3 * h * w)
+    check(lib().dcvc_frame_sse(x_hat.c(), src_u8.data_ptr(), uv_u8.data_ptr() if yuv else None, h, w, int(yuv),
+                               workspace.data_ptr(), out3.data_ptr(), stream()), "frame_sse")
+    return out3
 
 
 def qt_encode_step(y, params, sm, k, yhs, yhat, sym, idx, log_min, log_step):

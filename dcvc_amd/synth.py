@@ -34,3 +34,21 @@ def uniform_frame(h, w, t, seed=1):
 def to_float(frame_u8):
     """uint8 CHW -> float32 [0, 1], as PNGReader does (x / 255)."""
     return frame_u8.astype(np.float32) / np.float32(255.0)
+
+
+def moving_pattern_yuv420(h, w, t, seed=1, speed=2):
+    """The moving pattern as an 8-bit YUV420 source (config C4): BT.709
+    rgb_to_ycbcr420 (DCVC-DC/src/transforms/functional.py:16-39) rounded to
+    uint8, i.e. what a .yuv file of the sequence holds.  Returns (y (h, w),
+    uv (2, h/2, w/2))."""
+    rgb = moving_pattern(h, w, t, seed=seed, speed=speed).astype(np.float32) / 255
+    r, g, b = rgb[0:1], rgb[1:2], rgb[2:3]
+    kr, kg, kb = 0.2126, 0.7152, 0.0722
+    y = kr * r + kg * g + kb * b
+    cb = 0.5 * (b - y) / (1 - kb) + 0.5
+    cr = 0.5 * (r - y) / (1 - kr) + 0.5
+    cb = np.mean(np.reshape(cb, (1, h // 2, 2, w // 2, 2)), axis=(-1, -3))
+    cr = np.mean(np.reshape(cr, (1, h // 2, 2, w // 2, 2)), axis=(-1, -3))
+    uv = np.clip(np.concatenate((cb, cr), axis=0), 0, 1)
+    y = np.clip(y, 0, 1)
+    return np.round(y[0] * 255).astype(np.uint8), np.round(uv * 255).astype(np.uint8)

@@ -170,6 +170,29 @@ int dcvc_frame_to_nhwc(const uint8_t *src, int h, int w, dcvc_tensor y,
  * multiple of 64 (DCVC-HEM/test_video.py:113-119, F.pad mode="constant"). */
 int dcvc_frame_to_nhwc_zero_pad(const uint8_t *src, int h, int w, dcvc_tensor y,
                                 void *stream);
+/* YUV420 source frame (uint8 Y h x w, then U and V h/2 x w/2, the YUVReader
+ * layout, DCVC-DC/src/utils/video_reader.py:121-161) -> fp32 NHWC YCbCr 4:4:4
+ * in [0, 1], replicate-padded to out's size.  Chroma is upsampled as
+ * ycbcr420_to_444(order=0) does it (scipy.ndimage.zoom nearest,
+ * DCVC-DC/src/transforms/functional.py:61-72; test_video.py:111-112).  h, w
+ * even. */
+int dcvc_yuv420_to_nhwc(const uint8_t *y, const uint8_t *uv, int h, int w,
+                        dcvc_tensor out, void *stream);
+/* Bytes of device workspace dcvc_frame_sse needs. */
+int64_t dcvc_frame_sse_workspace(void);
+/* run_test's per-frame distortion (DCVC-DC/test_video.py:169-195): clamps
+ * x_hat (fp32 NHWC, 3 ch, padded) to [0, 1] IN PLACE, as recon_frame.clamp_
+ * does to the DPB frame, then writes to out3 (device, fp64) the squared-error
+ * sums over the top-left h x w crop against the uint8 source:
+ *   yuv420 = 0: per RGB channel, fp32 difference and square (PSNR(),
+ *               test_video.py:65-68); src = uint8 CHW, uv unused;
+ *   yuv420 = 1: Y, U, V of ycbcr444_to_420(x_hat) (functional.py:75-95)
+ *               against src = Y plane and uv = U|V planes, fp64 as calc_psnr
+ *               (src/utils/metrics.py:81-92).
+ * Summation order is fixed (deterministic). */
+int dcvc_frame_sse(dcvc_tensor x_hat, const uint8_t *src, const uint8_t *uv,
+                   int h, int w, int yuv420, double *workspace, double *out3,
+                   void *stream);
 
 /*
  * Quadtree (four-part) prior step k, encoder side

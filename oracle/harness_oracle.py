@@ -1,0 +1,93 @@
+"""run_test frame handling, CPU restatement — TEST INFRASTRUCTURE ONLY.
+
+Only tests/, ``__graft_entry__.smoke()`` and ``bench.py``'s cpu_baseline leg
+may import this module, as the checker.  The product path never imports it.
+
+numpy restatement of what DCVC-DC/test_video.py:108-195 does to a frame
+around the codec (paths relative to /root/reference/DCVC-DC):
+
+* ``ycbcr420_to_444`` with order=0 (src/transforms/functional.py:61-72):
+  ``scipy.ndimage.zoom(uv, (1, 2, 2), order=0)``, restated as the index map
+  ``round(i * (n - 1) / (2n - 1))``; tests pin the map against scipy itself.
+* ``np_image_to_tensor`` + ``F.pad(replicate)`` (test_video.py:56-62, 128-132).
+* ``ycbcr444_to_420`` (functional.py:75-95): float32 2x2 means, clip.
+* ``calc_psnr`` (src/utils/metrics.py:81-92) and ``PSNR`` (test_video.py:65-68).
+"""
+import numpy as np
+import torch
+
+
+def zoom_index(n_out, n_in):
+    """Nearest-neighbour source index of scipy.ndimage.zoom (order=0,
+    grid_mode=False) along one axis."""
+    if n_in <= 1:
+        return np.zeros(n_out, dtype=np.int64)
+    z = (n_in - 1) / (n_out - 1)
+    return np.floor(np.arange(n_out, dtype=np.float64) * z + 0.5).astype(np.int64)
+
+
+def ycbcr420_to_444_nearest(y, uv):
+    """y (1, h, w) float32, uv (2, h/2, w/2) float32 -> (3, h, w) float32."""
+    _, h, w = y.shape
+    ri = zoom_index(h, uv.shape[1])
+    ci = zoom_index(w, uv.shape[2])
+    up = uv[:, ri][:, :, ci]
+    return np.concatenate((y, up), axis=0)
+
+
+def yuv_u8_to_input(y_u8, uv_u8, H, W):
+    """uint8 planes -> (H, W, 3) float32 NHWC codec input, replicate-padded."""
+    y = y_u8.astype(np.float32)[None] / 255
+    uv = uv_u8.astype(np.float32) / 255
+    yuv = ycbcr420_to_444_nearest(y, uv)
+    h, w = yuv.shape[1:]
+    yuv = np.pad(yuv, ((0, 0), (0, H - h), (0, W - w)), mode="edge")
+    return np.ascontiguousarray(yuv.transpose(1, 2, 0))
+
+
+def ycbcr444_to_420(yuv):
+    """functional.py:75-95 (float32 in, float32 out)."""
+    c, h, w = yuv.shape
+    y, u, v = np.split(yuv, 3, axis=0)
+    u = np.mean(np.reshape(u, (1, h // 2, 2, w // 2, 2)), axis=(-1, -3))
+    v = np.mean(np.reshape(v, (1, h // 2, 2, w // 2, 2)), axis=(-1, -3))
+    uv = np.concatenate((u, v), axis=0)
+    return np.clip(y, 0., 1.), np.clip(uv, 0., 1.)
+
+
+def calc_psnr(img1, img2, data_range=255):
+    """metrics.py:81-92."""
+    img1 = img1.astype(np.float64)
+    img2 = img2.astype(np.float64)
+    mse = np.mean(np.square(img1 - img2))
+    if mse > 1e-10:
+        return 10 * np.log10(data_range * data_range / mse)
+    return 999.9
+
+
+def psnr_torch(a, b):
+    """test_video.py:65-68 on fp32 torch tensors."""
+    mse = torch.mean((a - b) ** 2)
+    return (20 * torch.log10(1 / torch.sqrt(mse))).item()
+
+
+def yuv_distortion(x_hat_chw, y_u8, uv_u8):
+    """(psnr_y, psnr_u, psnr_v, psnr) of a cropped, clamped 444 recon."""
+    y = y_u8.astype(np.float32) / 255
+    uv = uv_u8.astype(np.float32) / 255
+    y_rec, uv_rec = ycbcr444_to_420(x_hat_chw)
+    py = calc_psnr(y, y_rec[0], data_range=1)
+    pu = calc_psnr(uv[0], uv_rec[0], data_range=1)
+    pv = calc_psnr(uv[1], uv_rec[1], data_range=1)
+    return py, pu, pv, (6 * py + pu + pv) / 8
+
+
+def yuv_sse(x_hat_chw, y_u8, uv_u8):
+    """Per-plane fp64 squared-error sums behind yuv_distortion."""
+    y = y_u8.astype(np.float32) / 255
+    uv = uv_u8.astype(np.float32) / 255
+    y_rec, uv_rec = ycbcr444_to_420(x_hat_chw)
+    d = [y_rec[0].astype(np.float64) - y, uv_rec[0].astype(np.float64) - uv[0],
+         uv_rec[1].astype(np.float64) - uv[1]]
+    return np.array([np.sum(np.square(e)) for e in d])
+

@@ -4,13 +4,14 @@
 # by scripts/pmc_summary.py.  Output under gpurun_out/prof_<round>/; copy the
 # summaries into profiles/ to commit them.
 #   bash scripts/profile_round.sh r01
+#   PROF_ARGS=--yuv420 bash scripts/profile_round.sh r01_c4   (config C4)
 set -u
 cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
 R=${1:-r01}
 O=gpurun_out/prof_$R
 mkdir -p "$O"
-CMD=(python bench.py --steps ${PROF_STEPS:-6} --warmup 2 --no-cpu-baseline --no-roofline)
+CMD=(python bench.py --steps ${PROF_STEPS:-6} --warmup 2 --no-cpu-baseline --no-roofline ${PROF_ARGS:-})
 run() {  # name, rocprof args...
   local name=$1; shift
   timeout -k 10 600 rocprofv3 "$@" -d "$O/$name" -o run --output-format csv -- "${CMD[@]}" > "$O/$name.log" 2>&1

@@ -1,0 +1,229 @@
+"""run_test harness (DCVC-DC/test_video.py:71-237): YUV420 input conversion,
+in-place clamp, per-plane distortion and the JSON log.
+
+CPU tests pin the numpy restatement (oracle/harness_oracle.py) to the
+reference's own dependency (scipy.ndimage.zoom, numpy means) and check the
+log arithmetic.  GPU tests check the HIP kernels against that restatement
+(bit-exact input conversion, fp64 sums to 1e-12) and one YUV420 sequence of
+DCVC-DC through ``run_test`` against the CPU oracle codec (config C4's path at
+a small size; PSNR formula of test_video.py:171-181)."""
+import os
+import tempfile
+
+import numpy as np
+import pytest
+import scipy.ndimage
+import torch
+
+from oracle import harness_oracle as HO
+
+
+# --------------------------------------------------------------------- CPU
+@pytest.mark.parametrize("n", [1, 2, 3, 17, 50, 65, 68, 540, 1080, 1920])
+def test_zoom_index_matches_scipy(n):
+    src = np.arange(n, dtype=np.float64).reshape(1, n)
+    z = scipy.ndimage.zoom(src, (1, 2), order=0)
+    np.testing.assert_array_equal(z[0].astype(np.int64), HO.zoom_index(2 * n, n))
+
+
+def test_yuv_input_matches_reference_pipeline():
+    g = np.random.default_rng(3)
+    h, w = 38, 54
+    y = g.integers(0, 256, (h, w), dtype=np.uint8)
+    uv = g.integers(0, 256, (2, h // 2, w // 2), dtype=np.uint8)
+    # test_video.py:110-112 + functional.py:61-72 + F.pad(replicate), :128-132
+    yf = y.astype(np.float32)[None] / 255
+    uvf = uv.astype(np.float32) / 255
+    ref = np.concatenate((yf, scipy.ndimage.zoom(uvf, (1, 2, 2), order=0)), axis=0)
+    ref = torch.nn.functional.pad(torch.from_numpy(ref)[None], (0, 10, 0, 10), mode="replicate")[0]
+    ours = HO.yuv_u8_to_input(y, uv, h + 10, w + 10)
+    np.testing.assert_array_equal(ours, ref.permute(1, 2, 0).numpy())
+
+
+def test_chroma_mean_order():
+    """dcvc_frame_sse sums each 2x2 chroma block as (x00 + x01) + (x10 + x11),
+    the order numpy's float32 mean over axes (-1, -3) uses."""
+    g = np.random.default_rng(0)
+    a = g.random((1, 64, 2, 96, 2)).astype(np.float32)
+    m = np.mean(a, axis=(-1, -3))
+    s = (a[:, :, 0, :, 0] + a[:, :, 0, :, 1]) + (a[:, :, 1, :, 0] + a[:, :, 1, :, 1])
+    np.testing.assert_array_equal(m, s / np.float32(4))
+
+
+def test_psnr_formulas():
+    from dcvc_amd.harness import psnr_rgb, psnr_yuv, calc_psnr_from_sse
+    g = np.random.default_rng(1)
+    h, w = 20, 30
+    a = torch.from_numpy(g.random((1, 3, h, w)).astype(np.float32))
+    b = torch.from_numpy(g.random((1, 3, h, w)).astype(np.float32))
+    d = (a - b).numpy().astype(np.float32)
+    sse = np.array([np.sum((d[0, c].astype(np.float64)) ** 2) for c in range(3)])
+    assert abs(psnr_rgb(sse, h, w) - HO.psnr_torch(a, b)) < 1e-5
+    assert calc_psnr_from_sse(0.0, 10) == 999.9
+    x = g.random((3, h, w)).astype(np.float32)
+    yu8 = g.integers(0, 256, (h, w), dtype=np.uint8)
+    uvu8 = g.integers(0, 256, (2, h // 2, w // 2), dtype=np.uint8)
+    ours = psnr_yuv(HO.yuv_sse(x, yu8, uvu8), h, w)
+    np.testing.assert_allclose(ours, HO.yuv_distortion(x, yu8, uvu8), rtol=0, atol=1e-9)
+
+
+def test_generate_log_json_fields():
+    from dcvc_amd.harness import generate_log_json, generate_log_json_hem
+    types, bits, ps = [0, 1, 1, 0], [100, 40, 60, 120], [30.0, 29.0, 28.0, 31.0]
+    log = generate_log_json(4, 10, 1.5, types, bits, ps, [0.0] * 4)
+    assert log["i_frame_num"] == 2 and log["p_frame_num"] == 2
+    assert log["ave_i_frame_bpp"] == 220 / 2 / 10
+    assert log["ave_p_frame_bpp"] == 100 / 20
+    assert log["ave_all_frame_bpp"] == 320 / 40
+    assert log["ave_all_frame_psnr"] == sum(ps) / 4
+    assert "frame_bpp" not in log
+    yl = generate_log_json(4, 10, 1.5, types, bits, ps, [0.0] * 4, ps, ps, ps, [0.0] * 4, [0.0] * 4, [0.0] * 4)
+    assert yl["ave_p_frame_psnr_u"] == 28.5 and yl["ave_all_frame_psnr_v"] == sum(ps) / 4
+    hl = generate_log_json_hem(4, types, bits, ps, [0.0] * 4, 10, 1.5)
+    assert hl["frame_type"] == types and hl["frame_bpp"] == [10.0, 4.0, 6.0, 12.0]
+    assert "ave_i_frame_psnr_y" not in hl
+
+
+def test_yuv_reader_roundtrip(tmp_path):
+    from dcvc_amd.harness import YUVReader
+    g = np.random.default_rng(2)
+    h, w = 6, 8
+    frames = [(g.integers(0, 256, (h, w), dtype=np.uint8), g.integers(0, 256, (2, h // 2, w // 2), dtype=np.uint8))
+              for _ in range(3)]
+    p = tmp_path / "seq.yuv"
+    with open(p, "wb") as f:
+        for y, uv in frames:
+            f.write(y.tobytes())
+            f.write(uv.tobytes())
+    r = YUVReader(str(p)[:-4], w, h, skip_frame=1)   # the reader appends .yuv
+    for y, uv in frames[1:]:
+        ry, ruv = r.read_one_frame()
+        np.testing.assert_array_equal(ry, y)
+        np.testing.assert_array_equal(ruv, uv)
+    assert r.read_one_frame() == (None, None)
+    r.close()
+
+
+# --------------------------------------------------------------------- GPU
+gpu = pytest.mark.gpu
+
+
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+@gpu
+@pytest.mark.parametrize("shape", [(38, 54, 48, 64), (100, 130, 112, 144), (2160, 3840, 2160, 3840)])
+def test_yuv420_to_nhwc_bit_exact(shape):
+    _need_gpu()
+    from dcvc_amd import hip as K
+    h, w, H, W = shape
+    g = np.random.default_rng(h)
+    y = g.integers(0, 256, (h, w), dtype=np.uint8)
+    uv = g.integers(0, 256, (2, h // 2, w // 2), dtype=np.uint8)
+    out = K.empty(H, W, 3, K.F32)
+    K.yuv420_to_nhwc(torch.from_numpy(y).cuda(), torch.from_numpy(uv).cuda(), h, w, out)
+    np.testing.assert_array_equal(out.t().cpu().numpy(), HO.yuv_u8_to_input(y, uv, H, W))
+
+
+@gpu
+@pytest.mark.parametrize("yuv", [False, True])
+@pytest.mark.parametrize("shape", [(38, 54, 48, 64), (1080, 1920, 1088, 1920)])
+def test_frame_sse_and_inplace_clamp(yuv, shape):
+    _need_gpu()
+    from dcvc_amd import hip as K
+    h, w, H, W = shape
+    g = np.random.default_rng(w)
+    xh = torch.from_numpy((g.random((H, W, 3)) * 1.4 - 0.2).astype(np.float32)).cuda()
+    x_act = K.Act(xh.clone())
+    clamped = xh.clamp(0, 1).cpu().numpy()
+    ws = K.frame_sse_workspace(xh.device)
+    out = torch.zeros(3, dtype=torch.float64, device=xh.device)
+    crop = clamped[:h, :w].transpose(2, 0, 1)
+    if yuv:
+        y = g.integers(0, 256, (h, w), dtype=np.uint8)
+        uv = g.integers(0, 256, (2, h // 2, w // 2), dtype=np.uint8)
+        K.frame_sse(x_act, torch.from_numpy(y).cuda(), h, w, ws, out, uv_u8=torch.from_numpy(uv).cuda())
+        ref = HO.yuv_sse(np.ascontiguousarray(crop), y, uv)
+    else:
+        src = g.integers(0, 256, (3, h, w), dtype=np.uint8)
+        K.frame_sse(x_act, torch.from_numpy(src).cuda(), h, w, ws, out)
+        d = crop - src.astype(np.float32) / np.float32(255)
+        ref = np.array([np.sum((d[c] * d[c]).astype(np.float64)) for c in range(3)])
+    np.testing.assert_allclose(out.cpu().numpy(), ref, rtol=1e-12)
+    # recon_frame.clamp_(0, 1) acted on the whole padded buffer
+    np.testing.assert_array_equal(x_act.t().cpu().numpy(), clamped)
+
+
+def _oracle_sequence(i, p, xps, h, w, q):
+    """test_video.py's loop with the oracle codec and the C oracle coder."""
+    from oracle import rans_oracle as R
+    from tests.test_oracle_dc import oracle_tables, KIND
+    tabs = oracle_tables(i, p)
+    dpb, out = None, []
+    for t, xp in enumerate(xps):
+        pre = "i_" if t == 0 else "p_"
+        with torch.no_grad():
+            calls = i.compress(xp, False, q) if t == 0 else p.compress(xp, dpb, False, q, t % 4)
+            coder_calls = [(s.clamp(-30000, 30000).to(torch.int16).numpy(), ix.to(torch.int16).numpy(),
+                            tabs[pre + KIND[k]]) for k, s, ix in calls]
+            enc = R.DCStream()
+            stream = enc.encode(coder_calls)
+            decoded = enc.decode(stream)
+            pos = [0]
+
+            def decoder(kind, idx):
+                n = idx.numel()
+                v = decoded[pos[0]:pos[0] + n]
+                pos[0] += n
+                return v
+
+            if t == 0:
+                xh = i.decompress(decoder, h, w, False, q)
+                dpb = {"ref_frame": xh, "ref_feature": None, "ref_mv_feature": None, "ref_y": None, "ref_mv_y": None}
+            else:
+                dpb = p.decompress(dpb, decoder, h, w, False, q, t % 4)
+        dpb["ref_frame"].clamp_(0, 1)
+        out.append(((len(stream) + (13 if t == 0 else 6)) * 8, dpb["ref_frame"][0, :, :h, :w].numpy()))
+    return out
+
+
+@gpu
+def test_run_test_yuv420_matches_oracle(dc_golden):
+    """A YUV420 sequence (the C4 path at 100x130) through run_test in parity
+    precision: bits and PSNR_y/u/v against the oracle codec on the same
+    4:4:4 input, within the parity tolerance of tests/test_gpu_model_dc.py."""
+    _need_gpu()
+    from dcvc_amd.dc import DMC, IntraNoAR
+    from dcvc_amd.harness import run_test, ArrayReader
+    from dcvc_amd.layers import Precision
+    from dcvc_amd.synth import moving_pattern_yuv420
+    from oracle import dc_oracle as O
+    from oracle import rans_oracle as R
+    from tests.test_gpu_model_dc import PARITY_TOL
+    h, w, n, q = 100, 130, 3, 0
+    frames = [moving_pattern_yuv420(h, w, t, seed=5) for t in range(n)]
+    inet = IntraNoAR(precision=Precision.parity()).load_state_dict(dc_golden.i_state_dict())
+    pnet = DMC(precision=Precision.parity()).load_state_dict(dc_golden.p_state_dict())
+    inet.update(force=True)
+    pnet.update(force=True)
+    with tempfile.TemporaryDirectory() as td:
+        log = run_test(pnet, inet, {"frame_num": n, "gop_size": 32, "write_stream": True, "bin_folder": td,
+                                    "src_reader": ArrayReader(frames), "src_type": "yuv420",
+                                    "src_height": h, "src_width": w, "dist_in_yuv420": True,
+                                    "q_in_ckpt": False, "i_frame_q_index": q, "verbose": 1})
+    torch.set_num_threads(min(16, os.cpu_count() or 1))
+    io = O.IntraOracle(dc_golden.i_state_dict(), R.pmf_to_quantized_cdf)
+    po = O.DMCOracle(dc_golden.p_state_dict(), R.pmf_to_quantized_cdf)
+    H, W = 112, 144
+    xps = [torch.from_numpy(HO.yuv_u8_to_input(y, uv, H, W)).permute(2, 0, 1)[None].contiguous() for y, uv in frames]
+    ref = _oracle_sequence(io, po, xps, h, w, q)
+    for t, (bits, rec) in enumerate(ref):
+        py, pu, pv, p = HO.yuv_distortion(rec, *frames[t])
+        assert abs(log["frame_bpp"][t] * h * w - bits) / bits <= PARITY_TOL["bits_rel"], (t, log["frame_bpp"][t], bits)
+        assert abs(log["frame_psnr_y"][t] - py) <= PARITY_TOL["psnr_db"], t
+        assert abs(log["frame_psnr_u"][t] - pu) <= PARITY_TOL["psnr_db"], t
+        assert abs(log["frame_psnr_v"][t] - pv) <= PARITY_TOL["psnr_db"], t
+        assert abs(log["frame_psnr"][t] - p) <= PARITY_TOL["psnr_db"], t
+    assert log["i_frame_num"] == 1 and log["p_frame_num"] == n - 1
