@@ -49,6 +49,9 @@ def parse():
     ap.add_argument("--precision", choices=["fast", "parity"], default="fast")
     ap.add_argument("--stream_part", type=int, default=8,
                     help="rANS stream parts (the reference's --stream_part_i/p); parts code in parallel threads")
+    ap.add_argument("--lanes", type=int, default=1, choices=[1],
+                    help="GOP lanes per GPU.  Concurrent lanes (separate HIP streams / processes sharing the GPU) "
+                         "are disabled: co-running codecs showed an encoder/decoder divergence (DESIGN.md §9)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--profile-out", default="", help="per-shape kernel timing JSON of one P-frame")
@@ -264,82 +267,118 @@ def main():
     from dcvc_amd.harness import FrameStage, psnr_rgb, psnr_yuv
     from dcvc_amd.synth import moving_pattern, moving_pattern_yuv420
 
+    for kv in filter(None, os.environ.get("DCVC_OPTS", "").split(",")):
+        k, v = kv.split("=")
+        K.set_option(k, int(v))
     hem = args.model == "hem"
     isd, psd = make_weights(dist, rank, device, args.model)
     prec = Precision.fast(latent_compute=K.BF16) if args.precision == "fast" else Precision.parity()
     if hem:
         from dcvc_amd.hem import DMC, IntraNoAR
-        inet = IntraNoAR(precision=prec, device=device).load_state_dict(isd)
-        pnet = DMC(precision=prec, device=device).load_state_dict(psd)
         qi, qmv, qy = hem_q(isd, psd, args.rate)
     else:
         from dcvc_amd.dc import DMC, IntraNoAR
-        inet = IntraNoAR(precision=prec, stream_part=args.stream_part, device=device).load_state_dict(isd)
-        pnet = DMC(precision=prec, stream_part=args.stream_part, device=device).load_state_dict(psd)
-    inet.update(force=True)
-    pnet.update(force=True)
 
     h, w = args.height, args.width
     align = 64 if hem else 16     # HEM test_video.py:113-119 pads to 64, DC to 16
     nframes = args.warmup + args.steps
-    # run_test's frame handling (dcvc_amd.harness.FrameStage): uint8 source
-    # resident in HBM, converted to the padded NHWC input inside the step;
-    # the distortion (in-place clamp + squared-error sums) is part of the step
-    stage = FrameStage(h, w, align, args.yuv420, zero_pad=hem, frame_num=nframes + 2, device=device)
-    H, W = stage.H, stage.W
-    if args.yuv420:
-        frames = [tuple(torch.from_numpy(a).to(device) for a in moving_pattern_yuv420(h, w, t, seed=shard_seed(rank)))
-                  for t in range(nframes)]
-    else:
-        frames = [torch.from_numpy(moving_pattern(h, w, t, seed=shard_seed(rank))).to(device) for t in range(nframes)]
-    out_dir = f"/dev/shm/dcvc_bench_{os.getpid()}"
-    os.makedirs(out_dir, exist_ok=True)
-    state = {"dpb": None}
-    bits = []
-    kinds = []
+    out_root = f"/dev/shm/dcvc_bench_{os.getpid()}"
 
-    def step(i):
-        # uint8 source -> padded NHWC: replicate (DC test_video.py:130) / zeros (HEM)
-        x = stage.load(frames[i])
-        path = os.path.join(out_dir, f"{i}.bin")
-        if hem:
-            if i % args.gop == 0:
-                r = inet.encode_decode(x, qi, path, pic_width=w, pic_height=h)
-                state["dpb"] = {"ref_frame": r["x_hat"], "ref_feature": None, "ref_y": None, "ref_mv_y": None}
-                kinds.append("I")
+    class Lane:
+        """One GOP lane: its own codec instances, HIP stream, frame staging
+        and output folder.  Lane l codes GOP l of this rank's sequence (an
+        I-frame resets the DPB, so GOPs are independent, test_video.py:
+        140-150).  One lane per GPU: concurrent lanes (meant to overlap one
+        lane's host rANS work with another's kernels) are disabled until the
+        co-running divergence of DESIGN.md §9 is resolved."""
+
+        def __init__(self, l):
+            self.l = l
+            if hem:
+                self.inet = IntraNoAR(precision=prec, device=device).load_state_dict(isd)
+                self.pnet = DMC(precision=prec, device=device).load_state_dict(psd)
             else:
-                r = pnet.encode_decode(x, state["dpb"], path, pic_width=w, pic_height=h,
-                                       mv_y_q_scale=qmv, y_q_scale=qy)
-                state["dpb"] = r["dpb"]
-                kinds.append("P")
-        elif i % args.gop == 0:
-            r = inet.encode_decode(x, False, args.q_index, path, pic_width=w, pic_height=h)
-            state["dpb"] = {"ref_frame": r["x_hat"], "ref_feature": None, "ref_mv_feature": None,
-                            "ref_y": None, "ref_mv_y": None}
-            kinds.append("I")
-        else:
-            r = pnet.encode_decode(x, state["dpb"], False, args.q_index, path, pic_width=w, pic_height=h,
-                                   frame_idx=i % 4)
-            state["dpb"] = r["dpb"]
-            kinds.append("P")
-        bits.append(r["bit"])
-        stage.distortion(state["dpb"]["ref_frame"], frames[i], i)
+                self.inet = IntraNoAR(precision=prec, stream_part=args.stream_part, device=device).load_state_dict(isd)
+                self.pnet = DMC(precision=prec, stream_part=args.stream_part, device=device).load_state_dict(psd)
+            self.inet.update(force=True)
+            self.pnet.update(force=True)
+            self.stream = torch.cuda.current_stream(device)
+            # run_test's frame handling (dcvc_amd.harness.FrameStage): uint8
+            # source resident in HBM, converted to the padded NHWC input
+            # inside the step; the distortion (in-place clamp + squared-error
+            # sums) is part of the step
+            self.stage = FrameStage(h, w, align, args.yuv420, zero_pad=hem, frame_num=nframes + 2, device=device)
+            t0 = l * args.gop
+            if args.yuv420:
+                self.frames = [tuple(torch.from_numpy(a).to(device)
+                                     for a in moving_pattern_yuv420(h, w, t0 + t, seed=shard_seed(rank)))
+                               for t in range(nframes)]
+            else:
+                self.frames = [torch.from_numpy(moving_pattern(h, w, t0 + t, seed=shard_seed(rank))).to(device)
+                               for t in range(nframes)]
+            self.out_dir = os.path.join(out_root, str(l))
+            os.makedirs(self.out_dir, exist_ok=True)
+            self.dpb = None
+            self.bits, self.kinds, self.per = [], [], []
 
-    for i in range(args.warmup):
-        step(i)
+        def step(self, i):
+            # uint8 source -> padded NHWC: replicate (DC test_video.py:130) / zeros (HEM)
+            x = self.stage.load(self.frames[i])
+            path = os.path.join(self.out_dir, f"{i}.bin")
+            inet, pnet = self.inet, self.pnet
+            if hem:
+                if i % args.gop == 0:
+                    r = inet.encode_decode(x, qi, path, pic_width=w, pic_height=h)
+                    self.dpb = {"ref_frame": r["x_hat"], "ref_feature": None, "ref_y": None, "ref_mv_y": None}
+                    self.kinds.append("I")
+                else:
+                    r = pnet.encode_decode(x, self.dpb, path, pic_width=w, pic_height=h,
+                                           mv_y_q_scale=qmv, y_q_scale=qy)
+                    self.dpb = r["dpb"]
+                    self.kinds.append("P")
+            elif i % args.gop == 0:
+                r = inet.encode_decode(x, False, args.q_index, path, pic_width=w, pic_height=h)
+                self.dpb = {"ref_frame": r["x_hat"], "ref_feature": None, "ref_mv_feature": None,
+                            "ref_y": None, "ref_mv_y": None}
+                self.kinds.append("I")
+            else:
+                r = pnet.encode_decode(x, self.dpb, False, args.q_index, path, pic_width=w, pic_height=h,
+                                       frame_idx=i % 4)
+                self.dpb = r["dpb"]
+                self.kinds.append("P")
+            self.bits.append(r["bit"])
+            self.stage.distortion(self.dpb["ref_frame"], self.frames[i], i)
+
+        def run(self, lo, hi, timed):
+            with torch.cuda.device(device), torch.cuda.stream(self.stream):
+                for i in range(lo, hi):
+                    ts = time.time()
+                    self.step(i)
+                    if timed:
+                        self.per.append(time.time() - ts)
+                self.stream.synchronize()
+
+    lanes = [Lane(l) for l in range(args.lanes)]
+    H, W = lanes[0].stage.H, lanes[0].stage.W
+    torch.cuda.synchronize(device)   # setup work on the default stream is done before lanes start
+
+    def run_all(lo, hi, timed):
+        for ln in lanes:
+            ln.run(lo, hi, timed)
+
+    run_all(0, args.warmup, False)
     torch.cuda.synchronize(device)
     if dist is not None:
         dist.barrier()
     t0 = time.time()
-    per = []
-    for i in range(args.warmup, nframes):
-        ts = time.time()
-        step(i)
-        per.append(time.time() - ts)
+    run_all(args.warmup, nframes, True)
     torch.cuda.synchronize(device)
     if dist is not None:
         dist.barrier()
     elapsed = max_over_ranks(dist, time.time() - t0, device)
+
+    def step(i):   # one more frame on lane 0 (the roofline P-frame below)
+        lanes[0].run(i, i + 1, False)
 
     # ---- roofline of the dominant kernel, from per-launch HIP events recorded
     # on the stream the kernels run on, over one extra P-frame.  "Dominant" =
@@ -398,14 +437,16 @@ def main():
                                    "gbytes": round(sum(v[2] for v in shapes.values()) / 1e9, 2)}
 
     if rank == 0:
-        n_i = kinds[args.warmup:].count("I")
-        ti = [p for p, k in zip(per, kinds[args.warmup:]) if k == "I"]
-        tp = [p for p, k in zip(per, kinds[args.warmup:]) if k == "P"]
+        kinds = [k for ln in lanes for k in ln.kinds[args.warmup:nframes]]
+        per = [p for ln in lanes for p in ln.per]
+        n_i = kinds.count("I")
+        ti = [p for p, k in zip(per, kinds) if k == "I"]
+        tp = [p for p, k in zip(per, kinds) if k == "P"]
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             cpu = cpu_baseline_hem(isd, psd, args) if hem else cpu_baseline(isd, psd, args)
-        timed_bits = bits[args.warmup:nframes]
-        sse = stage.sums()[args.warmup:nframes]
+        timed_bits = [b for ln in lanes for b in ln.bits[args.warmup:nframes]]
+        sse = np.concatenate([ln.stage.sums()[args.warmup:nframes] for ln in lanes])
         if args.yuv420:
             per = [psnr_yuv(e, h, w) for e in sse]
             psnr = {"psnr": round(float(np.mean([p[3] for p in per])), 4),
@@ -415,7 +456,7 @@ def main():
         line = {
             "metric": f"encode+decode fps @{h}p per GPU ({'DCVC-HEM' if hem else 'DCVC-DC'} write mode, "
                       "real bitstreams)",
-            "value": round(world * args.steps / elapsed, 4),
+            "value": round(world * args.lanes * args.steps / elapsed, 4),
             "unit": "frames/s",
             "n_gpus": world,
             "steps": args.steps,
@@ -432,18 +473,20 @@ def main():
                                     else f"C3 DCVC-DC RGB {w}x{h} (pad {W}x{H}) IP={args.gop} write mode"),
                        "gop": args.gop, "precision": args.precision,
                        **({"rate": args.rate, "q_scales": [round(qi, 4), round(qmv, 4), round(qy, 4)]} if hem
-                          else {"q_index": args.q_index, "stream_part": args.stream_part}), "parallelism": f"sequence-sharded x{world}",
+                          else {"q_index": args.q_index, "stream_part": args.stream_part}), "parallelism": f"sequence-sharded x{world}, {args.lanes} GOP lane(s) per GPU",
+                       "lanes": args.lanes, "frames_timed": world * args.lanes * args.steps,
                        "I_frames_timed": n_i,
                        "ms_I": round(1e3 * float(np.mean(ti)), 2) if ti else None,
                        "ms_P": round(1e3 * float(np.mean(tp)), 2) if tp else None,
-                       "bpp": round(float(np.mean(timed_bits)) / (h * w), 5), **psnr},
+                       "bpp": round(float(np.mean(timed_bits)) / (h * w), 5), **psnr,
+                       **({"bits_per_lane": [int(sum(ln.bits[args.warmup:nframes])) for ln in lanes]}
+                          if args.lanes > 1 else {})},
             "roofline": roof,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
-    for f in os.listdir(out_dir):
-        os.remove(os.path.join(out_dir, f))
-    os.rmdir(out_dir)
+    import shutil
+    shutil.rmtree(out_root, ignore_errors=True)
     if dist is not None:
         dist.destroy_process_group()
 

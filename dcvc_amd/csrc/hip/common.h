@@ -55,6 +55,10 @@ __device__ __forceinline__ float apply_act(int act, float v, float slope) {
 // it ("conv3x3_kernel<48, 16, false, unsigned short>"), so per-launch HIP-event
 // timings can be matched to a rocprof kernel summary (dcvc_last_kernel).
 void dcvc_note_kernel(const char *fmt, ...);
+// Raise kern's dynamic-LDS limit to at least `bytes`, once per process and
+// under a lock: setting the attribute while another host thread launches the
+// same kernel on another stream (concurrent GOP lanes) is not safe.
+void dcvc_ensure_lds(const void *kern, int bytes);
 template <typename T> constexpr const char *tname();
 template <> constexpr const char *tname<float>() { return "float"; }
 template <> constexpr const char *tname<uint16_t>() { return "unsigned short"; }

@@ -22,8 +22,20 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <mutex>
+#include <unordered_map>
 
 static thread_local char g_last_kernel[192];
+
+void dcvc_ensure_lds(const void *kern, int bytes) {
+  static std::mutex mu;
+  static std::unordered_map<const void *, int> done;
+  std::lock_guard<std::mutex> lk(mu);
+  int &have = done[kern];
+  if (have >= bytes) return;
+  (void)hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+  have = bytes;
+}
 
 void dcvc_note_kernel(const char *fmt, ...) {
   va_list ap;
@@ -399,8 +411,7 @@ int launch(const ConvP &p0, hipStream_t st) {
   dcvc_note_kernel("conv_kernel<%s, %s, %s, %d, %d>@%lld", tname<TIN>(), tname<TOUT>(), bname(F32), BN, TH,
                    (long long)blocks * 256);
   if (lds > 64 * 1024)
-    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    dcvc_ensure_lds(reinterpret_cast<const void *>(kern), (int)lds);
   hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(256), lds, st, p);
   DCVC_LAUNCH_CHECK();
   return DCVC_HIP_OK;

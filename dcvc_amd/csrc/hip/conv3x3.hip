@@ -532,8 +532,7 @@ int launch_res(C3 p, hipStream_t st) {
     dcvc_note_kernel("conv3x3_res_kernel<%d, %s, %d, %d, %s, %s>@%lld", NCH, bname(TAIL), BN, TH, tname<TOUT>(),
                      bname(res), (long long)G * p.nblk_n * 256);
     if (lds > 64 * 1024)
-      (void)hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      dcvc_ensure_lds(reinterpret_cast<const void *>(kern), (int)lds);
     hipLaunchKernelGGL(kern, dim3((unsigned)(G * p.nblk_n)), dim3(256), lds, st, p);
     DCVC_LAUNCH_CHECK();
     return DCVC_HIP_OK;
@@ -622,8 +621,7 @@ int launch(C3 p, hipStream_t st) {
   dcvc_note_kernel("conv3x3_kernel<%d, %d, %s, %s>@%lld", BN, TH, bname(wsplit<BN, TH>()), tname<TOUT>(),
                    (long long)blocks * 256);
   if (lds > 64 * 1024)
-    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    dcvc_ensure_lds(reinterpret_cast<const void *>(kern), (int)lds);
   hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(256), lds, st, p);
   DCVC_LAUNCH_CHECK();
   return DCVC_HIP_OK;

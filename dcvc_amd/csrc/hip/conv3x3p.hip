@@ -410,8 +410,7 @@ int launch(P3 p, hipStream_t st) {
     auto kern = conv3p_kernel<CIN, BN, NW, RW, TOUT, SHUF>;
     dcvc_note_kernel("conv3p_kernel<%d, %d, %d, %d, %s, %s>@%lld", CIN, BN, NW, RW, tname<TOUT>(), bname(SHUF),
                      (long long)G * p.nblk_n * NW * 64);
-    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)G_::LDS);
+    dcvc_ensure_lds(reinterpret_cast<const void *>(kern), (int)G_::LDS);
     hipLaunchKernelGGL(kern, dim3((unsigned)(G * p.nblk_n)), dim3(NW * 64), G_::LDS, st, p);
     DCVC_LAUNCH_CHECK();
     return DCVC_HIP_OK;

@@ -415,8 +415,7 @@ int run(DcbP p, hipStream_t st) {
   dcvc_note_kernel("dcb_kernel<%d, %d, %s, %s>@%lld", CIN, COUT, bname(GATED), bname(ADAPT),
                    (long long)p.tiles_x * tiles_y * 256);
   if (lds > 64 * 1024)
-    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    dcvc_ensure_lds(reinterpret_cast<const void *>(kern), (int)lds);
   hipLaunchKernelGGL(kern, dim3((unsigned)(p.tiles_x * tiles_y)), dim3(256), lds, st, p);
   DCVC_LAUNCH_CHECK();
   return DCVC_HIP_OK;

@@ -420,8 +420,7 @@ int run(DcbP p, hipStream_t st) {
     const int G = g_cus;
     auto kern = dcbp_kernel<CIN, COUT, ADAPT>;
     dcvc_note_kernel("dcbp_kernel<%d, %d, %s>@%lld", CIN, COUT, bname(ADAPT), (long long)G * NTHR);
-    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)G_::LDS);
+    dcvc_ensure_lds(reinterpret_cast<const void *>(kern), (int)G_::LDS);
     hipLaunchKernelGGL(kern, dim3((unsigned)G), dim3(NTHR), G_::LDS, st, p);
     DCVC_LAUNCH_CHECK();
     return DCVC_HIP_OK;

@@ -221,8 +221,7 @@ int launch(G1 p, hipStream_t st) {
   dcvc_note_kernel("gemm1x1_kernel<%s, %s, %d, %d, %d>@%lld", tname<TIN>(), tname<TOUT>(), BM, BN, WMW,
                    (long long)p.tiles_m * tiles_n * 256);
   if (lds > 64 * 1024)
-    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    dcvc_ensure_lds(reinterpret_cast<const void *>(kern), (int)lds);
   hipLaunchKernelGGL(kern, dim3((unsigned)(p.tiles_m * tiles_n)), dim3(256), lds, st, p);
   DCVC_LAUNCH_CHECK();
   return DCVC_HIP_OK;

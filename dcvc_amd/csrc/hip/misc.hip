@@ -535,3 +535,52 @@ extern "C" int dcvc_sum_f32(const float *x, int64_t n, float *out, void *stream)
   DCVC_LAUNCH_CHECK();
   return DCVC_HIP_OK;
 }
+
+// ------------------------------------------------------------ debug aid
+// Fill the LDS of as many workgroups as fit on the chip with all-ones bytes
+// (bf16 / fp32 NaN).  LDS is not cleared between dispatches, so a kernel
+// launched next that reads LDS it never wrote sees NaN instead of whatever an
+// earlier kernel left there (scripts/lds_poison_check.py).
+__global__ void __launch_bounds__(256) lds_poison_kernel(int words) {
+  extern __shared__ uint32_t lds_words[];
+  for (int i = threadIdx.x; i < words; i += 256) lds_words[i] = 0xFFFFFFFFu;
+  __syncthreads();
+}
+
+extern "C" int dcvc_debug_poison_lds(int bytes, int blocks, void *stream) {
+  if (bytes <= 0 || bytes > 160 * 1024 || blocks <= 0) return DCVC_HIP_EINVAL;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  dcvc_ensure_lds(reinterpret_cast<const void *>(lds_poison_kernel), bytes);
+  hipLaunchKernelGGL(lds_poison_kernel, dim3(blocks), dim3(256), bytes, st, bytes / 4);
+  DCVC_LAUNCH_CHECK();
+  return DCVC_HIP_OK;
+}
+
+// Fill the VGPRs of as many waves as fit (8 per SIMD at 128 VGPRs each) with
+// all-ones bits: a kernel launched next that reads a register it never wrote
+// sees NaN (scripts/lds_poison_check.py --vgpr).
+__global__ void __launch_bounds__(256) vgpr_poison_kernel(int *sink) {
+#define P4(a) "v_mov_b32 v" #a "0, -1\n v_mov_b32 v" #a "1, -1\n v_mov_b32 v" #a "2, -1\n v_mov_b32 v" #a "3, -1\n" \
+              "v_mov_b32 v" #a "4, -1\n v_mov_b32 v" #a "5, -1\n v_mov_b32 v" #a "6, -1\n v_mov_b32 v" #a "7, -1\n" \
+              "v_mov_b32 v" #a "8, -1\n v_mov_b32 v" #a "9, -1\n"
+  asm volatile(P4(1) P4(2) P4(3) P4(4) P4(5) P4(6) P4(7) P4(8) P4(9) P4(10) P4(11) ::
+                   : "v10", "v11", "v12", "v13", "v14", "v15", "v16", "v17", "v18", "v19", "v20", "v21", "v22",
+                     "v23", "v24", "v25", "v26", "v27", "v28", "v29", "v30", "v31", "v32", "v33", "v34", "v35",
+                     "v36", "v37", "v38", "v39", "v40", "v41", "v42", "v43", "v44", "v45", "v46", "v47", "v48",
+                     "v49", "v50", "v51", "v52", "v53", "v54", "v55", "v56", "v57", "v58", "v59", "v60", "v61",
+                     "v62", "v63", "v64", "v65", "v66", "v67", "v68", "v69", "v70", "v71", "v72", "v73", "v74",
+                     "v75", "v76", "v77", "v78", "v79", "v80", "v81", "v82", "v83", "v84", "v85", "v86", "v87",
+                     "v88", "v89", "v90", "v91", "v92", "v93", "v94", "v95", "v96", "v97", "v98", "v99", "v100",
+                     "v101", "v102", "v103", "v104", "v105", "v106", "v107", "v108", "v109", "v110", "v111",
+                     "v112", "v113", "v114", "v115", "v116", "v117", "v118", "v119");
+#undef P4
+  if (threadIdx.x == 1024) *sink = 0;  // never true: keeps the kernel from being empty
+}
+
+extern "C" int dcvc_debug_poison_vgpr(int blocks, void *stream) {
+  if (blocks <= 0) return DCVC_HIP_EINVAL;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(vgpr_poison_kernel, dim3(blocks), dim3(256), 0, st, nullptr);
+  DCVC_LAUNCH_CHECK();
+  return DCVC_HIP_OK;
+}

@@ -39,8 +39,8 @@ class SymbolBuffer:
         return self.idx[self.offs[i]:self.offs[i + 1]]
 
     def to_host(self):
-        s = torch.empty(self.sym.numel(), dtype=self.sym_dtype, pin_memory=True)
-        x = torch.empty(self.idx.numel(), dtype=torch.int16, pin_memory=True)
+        s = K.pinned("sb_sym", self.sym.numel(), self.sym_dtype)
+        x = K.pinned("sb_idx", self.idx.numel(), torch.int16)
         s.copy_(self.sym, non_blocking=True)
         x.copy_(self.idx, non_blocking=True)
         torch.cuda.current_stream().synchronize()
@@ -105,8 +105,8 @@ class QuadtreePrior:
         yhat = K.empty(h, w, C, F32, dev)
         params = buf.ch(C, 3 * C)
         idx_d = torch.empty(n, dtype=torch.int16, device=dev)
-        idx_h = torch.empty(n, dtype=torch.int16, pin_memory=True)
-        sym_h = torch.empty(n, dtype=torch.int16, pin_memory=True)
+        idx_h = K.pinned("prior_idx", n, torch.int16)
+        sym_h = K.pinned("prior_sym", n, torch.int16)
         sym_d = torch.empty(n, dtype=torch.int16, device=dev)
         for k in range(4):
             sm = None if k == 0 else self.step_params(buf, k)

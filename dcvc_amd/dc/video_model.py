@@ -136,6 +136,10 @@ class DMC:
         self._zpad = {}
         if strict:
             ctx.check_strict([k for k in sd if k.startswith("bit_estimator") or "_q_" in k])
+        # weights were packed / uploaded on this thread's stream: finish before
+        # any other stream (a GOP lane) reads them
+        if torch.device(self.dev).type == "cuda":
+            torch.cuda.current_stream(self.dev).synchronize()
         return self
 
     # nn.Module calls test_video.py makes on the model (:301-302, :77)
@@ -362,10 +366,10 @@ class DMC:
         yh, yw = get_downsampled_shape(height, width, 16)
         mvz = ec.decode(self.mvz_table.indexes(zh, zw), self.mvz_table.table)
         z = ec.decode(self.z_table.indexes(zh, zw), self.z_table.table)
-        zs = torch.from_numpy(mvz.copy()).to(dev, non_blocking=True)
+        zs = K.upload(mvz, dev, "mv_z")
         mv_z_hat = K.empty(zh, zw, 64, F32, dev)
         K.from_symbols(zs, mv_z_hat)
-        zs2 = torch.from_numpy(z.copy()).to(dev, non_blocking=True)
+        zs2 = K.upload(z, dev, "z")
         z_hat = K.empty(zh, zw, G16, F32, dev)
         K.from_symbols(zs2, z_hat)
 
@@ -419,15 +423,15 @@ class DMC:
         if output_path is None:
             enc = self.forward_one_frame(x, dpb, q_in_ckpt=q_in_ckpt, q_index=q_index, frame_idx=frame_idx)
             return {"dpb": enc["dpb"], "bit": enc["bit"], "encoding_time": 0, "decoding_time": 0}
-        torch.cuda.synchronize(self.dev)
+        torch.cuda.current_stream(self.dev).synchronize()
         t0 = time.time()
         enc = self.compress(x, dpb, q_in_ckpt, q_index, frame_idx)
         encode_p(enc["bit_stream"], q_in_ckpt, q_index, frame_idx, output_path)
         bits = filesize(output_path) * 8
-        torch.cuda.synchronize(self.dev)
+        torch.cuda.current_stream(self.dev).synchronize()
         t1 = time.time()
         q_in_ckpt, q_index, frame_idx, string = decode_p(output_path)
         dec = self.decompress(dpb, string, pic_height, pic_width, q_in_ckpt, q_index, frame_idx)
-        torch.cuda.synchronize(self.dev)
+        torch.cuda.current_stream(self.dev).synchronize()
         t2 = time.time()
         return {"dpb": dec["dpb"], "bit": bits, "encoding_time": t1 - t0, "decoding_time": t2 - t1}

@@ -143,9 +143,8 @@ class FrameStage:
         """Host uint8 frame (CHW RGB, or (y, uv)) -> device tensors."""
         if self.yuv:
             y, uv = frame
-            return (torch.from_numpy(np.ascontiguousarray(y)).to(self.dev, non_blocking=True),
-                    torch.from_numpy(np.ascontiguousarray(uv)).to(self.dev, non_blocking=True))
-        return torch.from_numpy(np.ascontiguousarray(frame)).to(self.dev, non_blocking=True)
+            return K.upload(y, self.dev, "frame_y"), K.upload(uv, self.dev, "frame_uv")
+        return K.upload(frame, self.dev, "frame")
 
     def load(self, dframe):
         """Device uint8 frame -> padded NHWC fp32 codec input (test_video.py:

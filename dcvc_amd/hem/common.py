@@ -52,8 +52,8 @@ class DualPrior:
         n = buf.H * buf.W * (self.C // 2)
         yhat = K.empty(buf.H, buf.W, self.C, F32, dev)
         idx_d = torch.empty(n, dtype=torch.int16, device=dev)
-        idx_h = torch.empty(n, dtype=torch.int16, pin_memory=True)
-        sym_h = torch.empty(n, dtype=torch.int32, pin_memory=True)
+        idx_h = K.pinned("prior_idx", n, torch.int16)
+        sym_h = K.pinned("prior_sym", n, torch.int32)
         sym_d = torch.empty(n, dtype=torch.int32, device=dev)
         for k in range(2):
             sm = None if k == 0 else self.spatial(buf)

@@ -44,6 +44,10 @@ class IntraNoAR:
         self._q_cache = {}
         if strict:
             ctx.check_strict([k for k in sd if k.startswith("bit_estimator") or k.startswith("q_")])
+        # weights were packed / uploaded on this thread's stream: finish before
+        # any other stream (a GOP lane) reads them
+        if torch.device(self.dev).type == "cuda":
+            torch.cuda.current_stream(self.dev).synchronize()
         return self
 
     def to(self, device):

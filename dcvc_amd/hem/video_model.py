@@ -87,6 +87,10 @@ class DMC:
         self._zpad = {}
         if strict:
             ctx.check_strict([k for k in sd if k.startswith("bit_estimator") or "_q_" in k])
+        # weights were packed / uploaded on this thread's stream: finish before
+        # any other stream (a GOP lane) reads them
+        if torch.device(self.dev).type == "cuda":
+            torch.cuda.current_stream(self.dev).synchronize()
         return self
 
     def to(self, device):
@@ -287,7 +291,7 @@ class DMC:
         yh, yw = 4 * zh, 4 * zw  # the hyper decoders upsample z by 4 (HEM pads frames to 64)
         mvz = ec.decode(self.mvz_table.indexes(zh, zw).astype("int32"), self.mvz_table.table)
         mv_z_hat = K.empty(zh, zw, CH_MV, F32, dev)
-        K.from_symbols_i32(torch.from_numpy(mvz.copy()).to(dev, non_blocking=True), mv_z_hat)
+        K.from_symbols_i32(K.upload(mvz, dev, "mv_z"), mv_z_hat)
 
         def dec(idx):
             return ec.decode(idx.astype("int32"), st.table)
@@ -297,7 +301,7 @@ class DMC:
         c1, c2, c3 = self._motion_compensation(dpb, mv_hat)
         z = ec.decode(self.z_table.indexes(zh, zw).astype("int32"), self.z_table.table)
         z_hat = K.empty(zh, zw, CH_N, F32, dev)
-        K.from_symbols_i32(torch.from_numpy(z.copy()).to(dev, non_blocking=True), z_hat)
+        K.from_symbols_i32(K.upload(z, dev, "z"), z_hat)
         buf = self._y_params(z_hat, c3, dpb["ref_y"], yh, yw)
         y_hat = self.y_prior.decode(buf, yq, dec, st)
         x_hat, feature = self._recon(y_hat, c1, c2, c3)
@@ -339,8 +343,8 @@ class DMC:
         encode_p(enc["bit_stream"], mv_y_q_index, y_q_index, output_path)
         bits = filesize(output_path) * 8
         mv_y_q_index, y_q_index, string = decode_p(output_path)
-        torch.cuda.synchronize(self.dev)
+        torch.cuda.current_stream(self.dev).synchronize()
         start = time.time()
         dec = self.decompress(dpb, string, pic_height, pic_width, mv_y_q_index / 100, y_q_index / 100)
-        torch.cuda.synchronize(self.dev)
+        torch.cuda.current_stream(self.dev).synchronize()
         return {"dpb": dec["dpb"], "bit": bits, "decoding_time": time.time() - start}

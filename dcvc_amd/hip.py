@@ -6,6 +6,7 @@ the allocator and the stream provider; every computation below is one of our
 kernels.  Calls are asynchronous on the current HIP stream.
 """
 import ctypes
+import threading
 
 import numpy as np
 import torch
@@ -86,6 +87,8 @@ HIP_SYMBOLS = [
     ("dcvc_symbols_i32_to_nhwc", _i, [_vp, _T, _vp]),
     ("dcvc_se_scale", _i, [_T, _vp, _vp, _i, _vp, _vp, _vp]),
     ("dcvc_se_apply", _i, [_T, _T, _vp, _T, _vp]),
+    ("dcvc_debug_poison_lds", _i, [_i, _i, _vp]),
+    ("dcvc_debug_poison_vgpr", _i, [_i, _vp]),
 ]
 
 _L = None
@@ -128,6 +131,51 @@ def set_option(name, value):
 
 _raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None)
 _get_device = getattr(torch._C, "_cuda_getDevice", None)
+
+
+_tls = threading.local()
+
+
+def pinned(key, n, dtype):
+    """Persistent pinned host staging buffer of this host thread (first n
+    elements).  Freeing a pinned tensor whose async H2D copy may still be in
+    flight lets torch's process-wide pinned cache hand the block to another
+    thread (another GOP lane) that overwrites it; buffers that live as long as
+    the thread, reused only after a sync on the thread's stream, cannot race."""
+    d = getattr(_tls, "pinned", None)
+    if d is None:
+        d = _tls.pinned = {}
+    t = d.get((key, dtype))
+    if t is None or t.numel() < n:
+        if t is not None:
+            torch.cuda.current_stream().synchronize()  # no copy of the old buffer in flight
+        t = torch.empty(max(n, 1), dtype=dtype, pin_memory=True)
+        d[(key, dtype)] = t
+    return t[:n]
+
+
+def upload(arr, device, key):
+    """Host numpy array -> new device tensor, through this thread's pinned
+    staging buffer for `key` (async H2D on the current stream).  A pageable
+    source with non_blocking=True may be freed and reused by another host
+    thread before the DMA reads it; a pinned staging buffer is rewritten only
+    after its previous copy has completed (event per key)."""
+    arr = np.ascontiguousarray(arr)
+    d = getattr(_tls, "upload_ev", None)
+    if d is None:
+        d = _tls.upload_ev = {}
+    ev = d.get(key)
+    if ev is not None:
+        ev.synchronize()
+    dt = torch.from_numpy(arr.reshape(-1)[:0]).dtype
+    src = pinned(("upload", key), arr.size, dt)
+    src.numpy()[:] = arr.reshape(-1)
+    out = torch.empty(arr.shape, dtype=dt, device=device)
+    out.view(-1).copy_(src, non_blocking=True)
+    e = torch.cuda.Event()
+    e.record()
+    d[key] = e
+    return out
 
 
 def stream():
@@ -185,14 +233,46 @@ class Act:
 NULL_T = CTensor(None, 0, 0, 0, 0, 0, 0)
 
 
+# Debug aid (DCVC_CANARY=1): every Act is allocated with a 4 KiB tail filled
+# with a pattern; check_canaries() reports allocations whose tail a kernel
+# overwrote (an out-of-bounds store).
+CANARY = None
+_CANARY_BYTES = 4096
+
+
+def _alloc(H, W, C, dtype, dev, zero):
+    if CANARY is None:
+        f = torch.zeros if zero else torch.empty
+        return Act(f((H, W, C), dtype=_TORCH[dtype], device=dev))
+    import traceback
+    n = H * W * C
+    es = 4 if dtype == F32 else 2
+    flat = torch.empty(n * es + _CANARY_BYTES, dtype=torch.uint8, device=dev)
+    flat[n * es:].fill_(0xA5)
+    if zero:
+        flat[:n * es].zero_()
+    CANARY.append((flat, n * es, (H, W, C, dtype), "".join(traceback.format_stack(limit=6)[:-2])))
+    return Act(flat[:n * es].view(_TORCH[dtype]).view(H, W, C))
+
+
+def check_canaries():
+    bad = []
+    for flat, off, shape, where in CANARY or []:
+        tail = flat[off:]
+        if not bool((tail == 0xA5).all()):
+            first = int((tail != 0xA5).nonzero()[0])
+            bad.append((shape, first, where))
+    return bad
+
+
 def empty(H, W, C, dtype, device=None):
     dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
-    return Act(torch.empty((H, W, C), dtype=_TORCH[dtype], device=dev))
+    return _alloc(H, W, C, dtype, dev, False)
 
 
 def zeros(H, W, C, dtype, device=None):
     dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
-    return Act(torch.zeros((H, W, C), dtype=_TORCH[dtype], device=dev))
+    return _alloc(H, W, C, dtype, dev, True)
 
 
 def from_nchw(x, dtype=F32):

@@ -298,6 +298,15 @@ int dcvc_se_scale(dcvc_tensor x, const float *w1, const float *w2, int reduced,
 int dcvc_se_apply(dcvc_tensor a, dcvc_tensor x, const float *scale,
                   dcvc_tensor y, void *stream);
 
+/* Debug aid: fill the LDS of `blocks` workgroups with all-ones bytes (NaN in
+ * bf16 / fp32), to expose kernels that read LDS they never wrote
+ * (scripts/lds_poison_check.py).  Not used by the codec. */
+int dcvc_debug_poison_lds(int bytes, int blocks, void *stream);
+/* Debug aid: fill the VGPRs of `blocks` 256-thread workgroups (120 VGPRs per
+ * wave) with all-ones bits, to expose kernels that read registers they never
+ * wrote.  Not used by the codec. */
+int dcvc_debug_poison_vgpr(int blocks, void *stream);
+
 #ifdef __cplusplus
 }
 #endif
