@@ -130,6 +130,23 @@ __global__ void copy_kernel(View x, View y) {
   st<TY>(y.p, pix * y.cs + y.co + c, ld<TX>(x.p, ((int64_t)sy * x.W + sx) * x.cs + x.co + c));
 }
 
+// copy_kernel with 8 channels per thread (16/32-byte loads and stores) when
+// every channel count, stride and offset is a multiple of 8: the concat
+// copies of the contexts into the contextual encoder / recon inputs.
+template <typename TX, typename TY>
+__global__ void copy8_kernel(View x, View y) {
+  const int cg = y.C >> 3;
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (int64_t)y.H * y.W * cg) return;
+  const int c = (int)(idx % cg) * 8;
+  const int64_t pix = idx / cg;
+  const int py = (int)(pix / y.W), px = (int)(pix - (int64_t)py * y.W);
+  const int sy = min(py, x.H - 1), sx = min(px, x.W - 1);
+  float v[8];
+  V8<TX>::load(x.p, ((int64_t)sy * x.W + sx) * x.cs + x.co + c, v);
+  V8<TY>::store(y.p, pix * y.cs + y.co + c, v);
+}
+
 template <typename TY>
 __global__ void frame_kernel(const uint8_t *src, int h, int w, int zero_pad, View y) {
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -380,6 +397,15 @@ extern "C" int dcvc_add(dcvc_tensor a, dcvc_tensor b, dcvc_tensor y, void *strea
 
 static int copy_impl(dcvc_tensor x, dcvc_tensor y, void *stream) {
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (x.C % 8 == 0 && x.cstride % 8 == 0 && x.coff % 8 == 0 && y.cstride % 8 == 0 && y.coff % 8 == 0 &&
+      ((uintptr_t)x.ptr & 15) == 0 && ((uintptr_t)y.ptr & 15) == 0) {
+    const unsigned g8 = blocks_for((int64_t)y.H * y.W * (y.C / 8));
+#define K(TX, TY) hipLaunchKernelGGL((copy8_kernel<TX, TY>), dim3(g8), dim3(256), 0, st, mk(x), mk(y))
+    DISPATCH2(x.dtype, y.dtype, K);
+#undef K
+    DCVC_LAUNCH_CHECK();
+    return DCVC_HIP_OK;
+  }
   const unsigned g = blocks_for((int64_t)y.H * y.W * y.C);
 #define K(TX, TY) hipLaunchKernelGGL((copy_kernel<TX, TY>), dim3(g), dim3(256), 0, st, mk(x), mk(y))
   DISPATCH2(x.dtype, y.dtype, K);

@@ -104,7 +104,9 @@ class DMC:
         self.cf_c1out, self.cf_r1out = ctx.conv(cf + ".conv1_out"), ResBlock(ctx, cf + ".res_block1_out")
         # contextual encoder / decoder / recon (video_model.py:173-232)
         ce = "contextual_encoder"
-        self.ce_c1 = ctx.conv(ce + ".conv1", 2, cin_pad=56)
+        # buffer order cat(c1, x, 0 x5): the 48 context channels at offset 0
+        # (16-byte aligned copy), the reference's cat(x, c1) by input permutation
+        self.ce_c1 = ctx.conv(ce + ".conv1", 2, cin_pad=56, in_perm=list(range(3, 3 + G1)) + [0, 1, 2])
         self.ce_r1 = ResBlock(ctx, ce + ".res1", 0.1, True)
         self.ce_c2 = ctx.conv(ce + ".conv2", 2)
         self.ce_r2 = ResBlock(ctx, ce + ".res2", 0.1, True)
@@ -278,9 +280,9 @@ class DMC:
 
     def _contextual_encoder(self, x, c1, c2, c3, q):
         feat, dev = self.prec.feat, self.dev
-        cat = self._padded("ce", x.H, x.W, 56)                         # cat(x, c1, 0 x5)
-        K.copy(x, cat.ch(0, 3))
-        K.copy(c1, cat.ch(3, G1))
+        cat = self._padded("ce", x.H, x.W, 56)                         # cat(c1, x, 0 x5)
+        K.copy(c1, cat.ch(0, G1))
+        K.copy(x, cat.ch(G1, 3))
         cat2 = K.empty(c2.H, c2.W, G2 + G2, feat, dev)
         K.conv(self.ce_c1, cat, cat2.ch(0, G2))
         K.copy(c2, cat2.ch(G2, G2))

@@ -61,7 +61,9 @@ class DMC:
         self.cf_c2out, self.cf_r2out = ctx.conv(cf + ".conv2_out"), ResBlock(ctx, cf + ".res_block2_out")
         self.cf_c1out, self.cf_r1out = ctx.conv(cf + ".conv1_out"), ResBlock(ctx, cf + ".res_block1_out")
         ce = "contextual_encoder"
-        self.ce_c1 = ctx.conv(ce + ".conv1", 2, cin_pad=72)
+        # buffer order cat(context1, x, 0 x5), the reference's cat(x, context1)
+        # by input permutation (aligned 64-channel copy)
+        self.ce_c1 = ctx.conv(ce + ".conv1", 2, cin_pad=72, in_perm=list(range(3, 3 + CH_N)) + [0, 1, 2])
         self.ce_r1 = ResBlock(ctx, ce + ".res1", 0.1, True, True)
         self.ce_c2 = ctx.conv(ce + ".conv2", 2)
         self.ce_r2 = ResBlock(ctx, ce + ".res2", 0.1, True, True)
@@ -185,9 +187,9 @@ class DMC:
     def _contextual_encoder(self, x, c1, c2, c3, yq):
         """ContextualEncoder (:71-95), then y / curr_y_q."""
         feat, dev = self.prec.feat, self.dev
-        cat = self._padded("ce", x.H, x.W, 72)                          # cat(x, context1, 0 x5)
-        K.copy(x, cat.ch(0, 3))
-        K.copy(c1, cat.ch(3, CH_N))
+        cat = self._padded("ce", x.H, x.W, 72)                          # cat(context1, x, 0 x5)
+        K.copy(c1, cat.ch(0, CH_N))
+        K.copy(x, cat.ch(CH_N, 3))
         cat2 = K.empty(c2.H, c2.W, 2 * CH_N, feat, dev)
         K.conv(self.ce_c1, cat, cat2.ch(0, CH_N))
         K.copy(c2, cat2.ch(CH_N, CH_N))

@@ -62,17 +62,22 @@ class Ctx:
         if unused:
             raise RuntimeError(f"unexpected key(s) in state_dict: {sorted(unused)[:8]}")
 
-    def conv(self, name, stride=1, latent=False, compute=None, cin_pad=None, out_perm=None):
+    def conv(self, name, stride=1, latent=False, compute=None, cin_pad=None, out_perm=None, in_perm=None):
         """cin_pad: zero-pad the input channels to this count, for inputs whose
         concat buffer carries zero channels up to an 8-channel multiple (the
         kernels' 16-byte staging path); the products of the pad are exact
         zeros, so the result is unchanged.  out_perm: output channel order
         (a permutation of the reference's), so a producer can write a
-        consumer's concat layout directly; per-channel results are unchanged."""
+        consumer's concat layout directly; per-channel results are unchanged.
+        in_perm: input channel j of the buffer is the reference's input
+        channel in_perm[j] (a concat laid out with its 16-byte-aligned part
+        first); the sum over input channels is the same set of products."""
         if compute is None:
             compute = self.prec.latent_compute if latent else self.prec.feat_compute
         b = self.take(name + ".bias") if name + ".bias" in self.sd else None
         w = self.take(name + ".weight")
+        if in_perm is not None:
+            w = w.detach().float()[:, torch.as_tensor(in_perm, dtype=torch.long)]
         if cin_pad is not None and cin_pad > w.shape[1]:
             w = torch.nn.functional.pad(w.detach().float(), (0, 0, 0, 0, 0, cin_pad - w.shape[1]))
         if out_perm is not None:

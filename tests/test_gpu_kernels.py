@@ -535,3 +535,27 @@ def test_se_layer_matches_torch(dt, C, view):
     ref_y = a + x * ref_s[None, :, None, None]
     tol = 1e-5 if dt == "f32" else 1e-2
     assert rel_err(back(y), ref_y) < tol
+
+
+@pytest.mark.parametrize("src_dt,dst_dt", [(0, 0), (1, 1), (1, 0), (0, 1)])
+@pytest.mark.parametrize("coff,C,pad", [(8, 48, 0), (3, 48, 0), (64, 64, 0), (0, 16, 5)])
+def test_copy_and_pad_views(src_dt, dst_dt, coff, C, pad):
+    """dcvc_copy / dcvc_pad_replicate into a channel window of a wider buffer,
+    on the 8-channel vector path (aligned windows) and the scalar path: an
+    exact copy (with dtype conversion), replicate padding, other channels
+    untouched."""
+    k = K()
+    H, W = 37, 53
+    x = torch.randn(1, C, H, W)
+    xa = to_act(x, src_dt)
+    dst = k.zeros(H + pad, W + pad, coff + C + 8, dst_dt)
+    if pad:
+        k.pad_replicate(xa, dst.ch(coff, C))
+    else:
+        k.copy(xa, dst.ch(coff, C))
+    ref = F.pad(back(xa), (0, pad, 0, pad), mode="replicate")
+    if dst_dt == 1:
+        ref = ref.to(torch.bfloat16).float()
+    got = dst.t().float().cpu()
+    assert torch.equal(got[:, :, coff:coff + C].permute(2, 0, 1).unsqueeze(0), ref)
+    assert not got[:, :, :coff].any() and not got[:, :, coff + C:].any()
