@@ -384,9 +384,10 @@ __global__ void __launch_bounds__(NW * 64) conv3p_kernel(P3 p) {
 
 int g_cus = 0;
 int g_enabled = 1;
+int g_occ = 1;  // dcvc_set_option("conv3x3_occupancy", 2): two 8-row workgroups per CU where they fit
 
 template <int CIN, int BN, int NW, int RW, typename TOUT, bool SHUF>
-int launch(P3 p, hipStream_t st) {
+int launch(P3 p, hipStream_t st, int per_cu = 1) {
   typedef Geo<CIN, BN, NW, RW> G_;
   if constexpr (G_::LDS > 160 * 1024) {
     return DCVC_HIP_EUNSUPPORTED;
@@ -404,7 +405,7 @@ int launch(P3 p, hipStream_t st) {
     }
     // a grid of fewer tiles than CUs is better served per tile
     if (ntiles * p.nblk_n < g_cus) return DCVC_HIP_EUNSUPPORTED;
-    int64_t G = g_cus / p.nblk_n;
+    int64_t G = (int64_t)g_cus * per_cu / p.nblk_n;
     if (G > ntiles) G = ntiles;
     if (G < 1) G = 1;
     auto kern = conv3p_kernel<CIN, BN, NW, RW, TOUT, SHUF>;
@@ -420,6 +421,9 @@ int launch(P3 p, hipStream_t st) {
 // 16 output rows per tile (8 waves x 2) when the LDS holds it, else 8.
 template <int CIN, int BN, typename TOUT, bool SHUF>
 int pick_th(const P3 &p, hipStream_t st) {
+  if constexpr (2 * Geo<CIN, BN, 8, 1>::LDS <= 160 * 1024) {
+    if (g_occ >= 2) return launch<CIN, BN, 8, 1, TOUT, SHUF>(p, st, 2);
+  }
   if constexpr (Geo<CIN, BN, 8, 2>::LDS <= 160 * 1024) return launch<CIN, BN, 8, 2, TOUT, SHUF>(p, st);
   return launch<CIN, BN, 8, 1, TOUT, SHUF>(p, st);
 }
@@ -512,3 +516,4 @@ extern "C" int dcvc_internal_conv3p(const dcvc_conv_args *a, void *stream) {
 
 // dcvc_set_option("conv3x3_persistent", 0/1) (A/B switch, via conv.hip)
 extern "C" void dcvc_internal_conv3p_enable(int v) { g_enabled = v; }
+extern "C" void dcvc_internal_conv3p_occupancy(int v) { g_occ = v; }

@@ -11,8 +11,10 @@ distortion with ``dcvc_frame_sse``, which also performs
 sums stay on the device until the end of the sequence (one transfer), and the
 PSNR formulas are evaluated on the host exactly as the reference writes them.
 
-MS-SSIM (``calc_ssim``; DCVC-HEM always computes it) needs the
-``pytorch_msssim`` package for RGB, which is absent from this image; it is
+MS-SSIM: for YUV420 sources ``calc_ssim`` runs the reference's per-plane
+``calc_msssim`` (src/utils/metrics.py:39-62) on the GPU in fp64 (``MsSsim``,
+msssim.hip).  RGB MS-SSIM is ``pytorch_msssim.ms_ssim`` in the reference (DC
+and HEM), a package absent from this image, so it cannot be pinned: it is
 reported as 0 with ``msssim_unavailable`` set in the log.
 """
 import os
@@ -169,6 +171,65 @@ class FrameStage:
         return self.sse.cpu().numpy()
 
 
+class MsSsim:
+    """calc_msssim (DCVC-DC/src/utils/metrics.py:39-62) of the three planes of
+    a YUV420 frame, test_video.py:182-185: per level, the means of the ssim
+    and cs maps on the GPU (dcvc_ssim_level), the 2x2 reflect downsample
+    (dcvc_down2_f64); the weighted product on the host."""
+
+    W5 = np.array([0.0448, 0.2856, 0.3001, 0.2363, 0.1333])
+    W4 = np.array([0.0517, 0.3295, 0.3462, 0.2726])
+
+    def __init__(self, h, w, frame_num, device):
+        if min(h // 2, w // 2) < 88:
+            raise ValueError("calc_msssim needs planes of at least 88 x 88 (metrics.py:49-50)")
+        self.h, self.w, self.dev = h, w, device
+        n = h * w + 2 * (h // 2) * (w // 2)
+        self.src = torch.empty(n, dtype=torch.float64, device=device)
+        self.rec = torch.empty(n, dtype=torch.float64, device=device)
+        x, y = np.mgrid[-5:6, -5:6]                         # fspecial_gauss(11, 1.5), metrics.py:9-12
+        g = np.exp(-((x ** 2 + y ** 2) / (2.0 * 1.5 ** 2)))
+        self.win = torch.from_numpy(g / g.sum()).to(device)
+        self.ws = torch.empty(int(K.lib().dcvc_ssim_workspace()) // 8, dtype=torch.float64, device=device)
+        self.out = torch.zeros((max(frame_num, 1), 3, 5, 2), dtype=torch.float64, device=device)
+        self.planes = []                                    # (offset, ph, pw, levels, level buffers)
+        off = 0
+        for ph, pw in ((h, w), (h // 2, w // 2), (h // 2, w // 2)):
+            L = 5 if ph >= 176 and pw >= 176 else 4
+            bufs, sh, sw = [], ph, pw
+            for _ in range(L - 1):
+                sh, sw = (sh + 1) // 2, (sw + 1) // 2
+                bufs.append((torch.empty(sh * sw, dtype=torch.float64, device=device),
+                             torch.empty(sh * sw, dtype=torch.float64, device=device), sh, sw))
+            self.planes.append((off, ph, pw, L, bufs))
+            off += ph * pw
+
+    def run(self, x_hat, y_u8, uv_u8, slot):
+        K.yuv_planes_f64(x_hat, y_u8, uv_u8, self.h, self.w, self.src, self.rec)
+        for p, (off, ph, pw, L, bufs) in enumerate(self.planes):
+            a, b, sh, sw = self.src[off:off + ph * pw], self.rec[off:off + ph * pw], ph, pw
+            for k in range(L):
+                K.ssim_level(a, b, sh, sw, self.win, self.ws, self.out[slot, p, k])
+                if k < L - 1:
+                    na, nb, nh, nw = bufs[k]
+                    K.down2_f64(a, sh, sw, na)
+                    K.down2_f64(b, sh, sw, nb)
+                    a, b, sh, sw = na, nb, nh, nw
+
+    def values(self, n):
+        """(msssim_y, msssim_u, msssim_v, (6 y + u + v) / 8) per frame."""
+        o = self.out[:n].cpu().numpy()
+        res = []
+        for f in range(n):
+            v = []
+            for p, (_, _, _, L, _) in enumerate(self.planes):
+                wgt = self.W5 if L == 5 else self.W4
+                mssim, mcs = o[f, p, :L, 0], o[f, p, :L, 1]
+                v.append(float(np.prod(mcs[0:L - 1] ** wgt[0:L - 1]) * (mssim[L - 1] ** wgt[L - 1])))
+            res.append((v[0], v[1], v[2], (6 * v[0] + v[1] + v[2]) / 8))
+        return res
+
+
 def psnr_rgb(sse3, h, w):
     """PSNR() of test_video.py:65-68: mse = mean((x_hat - x)^2) as an fp32
     tensor, psnr = 20 * log10(1 / sqrt(mse)) in fp32."""
@@ -287,6 +348,7 @@ def run_test(p_frame_net, i_frame_net, args):
     reader = _reader(args, yuv)
     h, w = args["src_height"], args["src_width"]
     stage = FrameStage(h, w, 16, yuv, zero_pad=False, frame_num=frame_num, device=device)
+    ms = MsSsim(h, w, frame_num, device) if (yuv and args.get("calc_ssim")) else None
     frame_types, bits = [], []
     start_time = time.time()
     p_frame_number = 0
@@ -319,6 +381,9 @@ def run_test(p_frame_net, i_frame_net, args):
                 dec_t += result["decoding_time"]
             bits.append(result["bit"])
             stage.distortion(recon, dframe, frame_idx)
+            if ms is not None:
+                from .dc.video_model import as_act
+                ms.run(as_act(recon), dframe[0], dframe[1], frame_idx)
             if verbose >= 2:
                 print(f"frame {frame_idx}, bits: {bits[-1]:.3f}", flush=True)
     sse = stage.sums()
@@ -330,14 +395,15 @@ def run_test(p_frame_net, i_frame_net, args):
     zeros = [0.0] * frame_num
     if yuv:
         per = [psnr_yuv(sse[i], h, w) for i in range(frame_num)]
-        log = generate_log_json(frame_num, h * w, test_time, frame_types, bits, [p[3] for p in per], zeros,
-                                [p[0] for p in per], [p[1] for p in per], [p[2] for p in per],
-                                zeros, zeros, zeros, verbose=verbose >= 1)
+        mv = ms.values(frame_num) if ms is not None else [(0.0, 0.0, 0.0, 0.0)] * frame_num
+        log = generate_log_json(frame_num, h * w, test_time, frame_types, bits, [p[3] for p in per],
+                                [m[3] for m in mv], [p[0] for p in per], [p[1] for p in per], [p[2] for p in per],
+                                [m[0] for m in mv], [m[1] for m in mv], [m[2] for m in mv], verbose=verbose >= 1)
     else:
         psnrs = [psnr_rgb(sse[i], h, w) for i in range(frame_num)]
         log = generate_log_json(frame_num, h * w, test_time, frame_types, bits, psnrs, zeros,
                                 verbose=verbose >= 1)
-    if args.get("calc_ssim"):
+    if args.get("calc_ssim") and not yuv:
         log["msssim_unavailable"] = True
     return log
 

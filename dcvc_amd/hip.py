@@ -87,6 +87,10 @@ HIP_SYMBOLS = [
     ("dcvc_symbols_i32_to_nhwc", _i, [_vp, _T, _vp]),
     ("dcvc_se_scale", _i, [_T, _vp, _vp, _i, _vp, _vp, _vp]),
     ("dcvc_se_apply", _i, [_T, _T, _vp, _T, _vp]),
+    ("dcvc_yuv_planes_f64", _i, [_T, _vp, _vp, _i, _i, _vp, _vp, _vp]),
+    ("dcvc_ssim_workspace", ctypes.c_int64, []),
+    ("dcvc_ssim_level", _i, [_vp, _vp, _i, _i, _vp, ctypes.c_double, ctypes.c_double, _vp, _vp, _vp]),
+    ("dcvc_down2_f64", _i, [_vp, _i, _i, _vp, _vp]),
     ("dcvc_debug_poison_lds", _i, [_i, _i, _vp]),
     ("dcvc_debug_poison_vgpr", _i, [_i, _vp]),
 ]
@@ -471,6 +475,24 @@ def frame_sse(x_hat, src_u8, h, w, workspace, out3, uv_u8=None):
     check(lib().dcvc_frame_sse(x_hat.c(), src_u8.data_ptr(), uv_u8.data_ptr() if yuv else None, h, w, int(yuv),
                                workspace.data_ptr(), out3.data_ptr(), stream()), "frame_sse")
     return out3
+
+
+def yuv_planes_f64(x_hat, y_u8, uv_u8, h, w, src, rec):
+    """fp64 source / recon planes [Y | U | V] of the crop (calc_msssim's inputs)."""
+    n = h * w + 2 * (h // 2) * (w // 2)
+    assert src.dtype == torch.float64 and rec.dtype == torch.float64 and src.numel() >= n and rec.numel() >= n
+    check(lib().dcvc_yuv_planes_f64(x_hat.c(), y_u8.data_ptr(), uv_u8.data_ptr(), h, w, src.data_ptr(),
+                                    rec.data_ptr(), stream()), "yuv_planes_f64")
+
+
+def ssim_level(a, b, h, w, window, workspace, out2):
+    """Means of calc_ssim's ssim and cs maps of two fp64 h x w planes."""
+    check(lib().dcvc_ssim_level(a.data_ptr(), b.data_ptr(), h, w, window.data_ptr(), 1e-4, 9e-4,
+                                workspace.data_ptr(), out2.data_ptr(), stream()), "ssim_level")
+
+
+def down2_f64(x, h, w, y):
+    check(lib().dcvc_down2_f64(x.data_ptr(), h, w, y.data_ptr(), stream()), "down2_f64")
 
 
 def qt_encode_step(y, params, sm, k, yhs, yhat, sym, idx, log_min, log_step):

@@ -298,6 +298,26 @@ int dcvc_se_scale(dcvc_tensor x, const float *w1, const float *w2, int reduced,
 int dcvc_se_apply(dcvc_tensor a, dcvc_tensor x, const float *scale,
                   dcvc_tensor y, void *stream);
 
+/* MS-SSIM of the YUV420 path (calc_msssim, DCVC-DC/src/utils/metrics.py:15-62,
+ * called per plane at test_video.py:182-184), fp64 as the reference computes
+ * it.  dcvc_yuv_planes_f64 writes calc_msssim's inputs: the uint8/255 source
+ * planes and the clamped recon's ycbcr444_to_420 planes of the h x w crop,
+ * each as [Y h*w | U | V (h/2)*(w/2)] doubles.  dcvc_ssim_level writes to
+ * out2 the means of calc_ssim's ssim and cs maps for two h x w planes
+ * (11x11 'valid' Gaussian window `window121`, C1/C2 for data_range 1);
+ * workspace: dcvc_ssim_workspace() bytes.  dcvc_down2_f64 is the
+ * ndimage.convolve(ones(2,2)/4, mode='reflect')[::2, ::2] step between levels
+ * (out: ceil(h/2) x ceil(w/2)).  The level loop and the final weighted
+ * product run on the host. */
+int dcvc_yuv_planes_f64(dcvc_tensor x_hat, const uint8_t *y, const uint8_t *uv,
+                        int h, int w, double *src_planes, double *rec_planes,
+                        void *stream);
+int64_t dcvc_ssim_workspace(void);
+int dcvc_ssim_level(const double *a, const double *b, int h, int w,
+                    const double *window121, double C1, double C2,
+                    double *workspace, double *out2, void *stream);
+int dcvc_down2_f64(const double *in, int h, int w, double *out, void *stream);
+
 /* Debug aid: fill the LDS of `blocks` workgroups with all-ones bytes (NaN in
  * bf16 / fp32), to expose kernels that read LDS they never wrote
  * (scripts/lds_poison_check.py).  Not used by the codec. */

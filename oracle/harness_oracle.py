@@ -91,3 +91,66 @@ def yuv_sse(x_hat_chw, y_u8, uv_u8):
          uv_rec[1].astype(np.float64) - uv[1]]
     return np.array([np.sum(np.square(e)) for e in d])
 
+
+
+# --------------------------------------------------------------- MS-SSIM
+def fspecial_gauss(size=11, sigma=1.5):
+    """metrics.py:9-12."""
+    x, y = np.mgrid[-size // 2 + 1:size // 2 + 1, -size // 2 + 1:size // 2 + 1]
+    g = np.exp(-((x ** 2 + y ** 2) / (2.0 * sigma ** 2)))
+    return g / g.sum()
+
+
+def _filter_valid(win, img):
+    """fftconvolve(window, img, 'valid') restated as the direct 'valid'
+    correlation with the flipped window (same linear map)."""
+    k = win[::-1, ::-1]
+    h, w = img.shape
+    out = np.zeros((h - 10, w - 10))
+    for ky in range(11):
+        for kx in range(11):
+            out += k[ky, kx] * img[ky:ky + h - 10, kx:kx + w - 10]
+    return out
+
+
+def calc_ssim(img1, img2, data_range=1.0):
+    """metrics.py:15-36 (means of the ssim and cs maps)."""
+    img1 = img1.astype(np.float64)
+    img2 = img2.astype(np.float64)
+    win = fspecial_gauss(11, 1.5)
+    C1, C2 = (0.01 * data_range) ** 2, (0.03 * data_range) ** 2
+    mu1, mu2 = _filter_valid(win, img1), _filter_valid(win, img2)
+    m1s, m2s, m12 = mu1 * mu1, mu2 * mu2, mu1 * mu2
+    s1 = _filter_valid(win, img1 * img1) - m1s
+    s2 = _filter_valid(win, img2 * img2) - m2s
+    s12 = _filter_valid(win, img1 * img2) - m12
+    ssim = ((2 * m12 + C1) * (2 * s12 + C2)) / ((m1s + m2s + C1) * (s1 + s2 + C2))
+    cs = (2.0 * s12 + C2) / (s1 + s2 + C2)
+    return ssim.mean(), cs.mean()
+
+
+def down2_reflect(im):
+    """ndimage.convolve(im, ones((2,2))/4, mode='reflect')[::2, ::2]
+    (metrics.py:54-59): 2x2 means, the row/column past an odd edge reflecting
+    to the edge."""
+    h, w = im.shape
+    p = np.pad(im, ((0, h % 2), (0, w % 2)), mode="edge")
+    return ((p[0::2, 0::2] + p[0::2, 1::2]) + p[1::2, 0::2] + p[1::2, 1::2]) * 0.25
+
+
+def calc_msssim(img1, img2, data_range=1.0):
+    """metrics.py:39-62."""
+    level, weight = 5, np.array([0.0448, 0.2856, 0.3001, 0.2363, 0.1333])
+    h, w = img1.shape
+    if h < 176 or w < 176:
+        level, weight = 4, np.array([0.0517, 0.3295, 0.3462, 0.2726])
+    assert h >= 88 and w >= 88
+    im1, im2 = img1.astype(np.float64), img2.astype(np.float64)
+    mssim, mcs = [], []
+    for _ in range(level):
+        s, c = calc_ssim(im1, im2, data_range)
+        mssim.append(s)
+        mcs.append(c)
+        im1, im2 = down2_reflect(im1), down2_reflect(im2)
+    mssim, mcs = np.array(mssim), np.array(mcs)
+    return np.prod(mcs[0:level - 1] ** weight[0:level - 1]) * (mssim[level - 1] ** weight[level - 1])

@@ -227,3 +227,100 @@ def test_run_test_yuv420_matches_oracle(dc_golden):
         assert abs(log["frame_psnr_v"][t] - pv) <= PARITY_TOL["psnr_db"], t
         assert abs(log["frame_psnr"][t] - p) <= PARITY_TOL["psnr_db"], t
     assert log["i_frame_num"] == 1 and log["p_frame_num"] == n - 1
+
+
+# ------------------------------------------------------------------ MS-SSIM
+def _golden_msssim():
+    import importlib.util
+    import json
+    here = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+    spec = importlib.util.spec_from_file_location("make_golden_msssim", os.path.join(here, "make_golden_msssim.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    with open(os.path.join(here, "msssim_golden.json")) as f:
+        return m.planes, json.load(f)["cases"]
+
+
+def test_down2_reflect_matches_scipy():
+    import scipy.ndimage as nd
+    g = np.random.default_rng(4)
+    for h, w in ((5, 7), (6, 8), (11, 10)):
+        a = g.random((h, w))
+        ref = nd.convolve(a, np.ones((2, 2)) / 4.0, mode="reflect")[::2, ::2]
+        np.testing.assert_allclose(HO.down2_reflect(a), ref, rtol=0, atol=1e-15)
+
+
+def test_msssim_oracle_matches_reference_fixtures():
+    """oracle calc_msssim vs the reference's own calc_msssim outputs
+    (tests/golden/make_golden_msssim.py imported metrics.py)."""
+    planes, cases = _golden_msssim()
+    for c in cases[:4]:
+        src, rec = planes(c["seed"], c["h"], c["w"])
+        assert abs(HO.calc_msssim(src, rec) - c["msssim"]) < 1e-12, c
+        assert abs(HO.calc_psnr(src, rec, data_range=1) - c["psnr"]) < 1e-9, c
+
+
+def _gpu_msssim(a, b):
+    """calc_msssim of two host planes through dcvc_ssim_level / dcvc_down2_f64."""
+    from dcvc_amd import hip as K
+    from dcvc_amd.harness import MsSsim
+    dev = torch.device("cuda", 0)
+    h, w = a.shape
+    x, y = np.mgrid[-5:6, -5:6]
+    g = np.exp(-((x ** 2 + y ** 2) / (2.0 * 1.5 ** 2)))
+    win = torch.from_numpy(g / g.sum()).to(dev)
+    ws = torch.empty(int(K.lib().dcvc_ssim_workspace()) // 8, dtype=torch.float64, device=dev)
+    L = 5 if h >= 176 and w >= 176 else 4
+    out = torch.zeros((L, 2), dtype=torch.float64, device=dev)
+    ta = torch.from_numpy(a.astype(np.float64).reshape(-1)).to(dev)
+    tb = torch.from_numpy(b.astype(np.float64).reshape(-1)).to(dev)
+    for k in range(L):
+        K.ssim_level(ta, tb, h, w, win, ws, out[k])
+        if k < L - 1:
+            nh, nw = (h + 1) // 2, (w + 1) // 2
+            na = torch.empty(nh * nw, dtype=torch.float64, device=dev)
+            nb = torch.empty(nh * nw, dtype=torch.float64, device=dev)
+            K.down2_f64(ta, h, w, na)
+            K.down2_f64(tb, h, w, nb)
+            ta, tb, h, w = na, nb, nh, nw
+    o = out.cpu().numpy()
+    wgt = MsSsim.W5 if L == 5 else MsSsim.W4
+    return float(np.prod(o[:L - 1, 1] ** wgt[:L - 1]) * o[L - 1, 0] ** wgt[L - 1])
+
+
+@gpu
+def test_gpu_msssim_matches_reference_fixtures():
+    """The GPU level chain against the reference's calc_msssim outputs (fp64;
+    the reference filters with fftconvolve, the GPU sums directly: agreement
+    to 1e-10)."""
+    _need_gpu()
+    planes, cases = _golden_msssim()
+    for c in cases:
+        src, rec = planes(c["seed"], c["h"], c["w"])
+        assert abs(_gpu_msssim(src, rec) - c["msssim"]) < 1e-10, c
+
+
+@gpu
+def test_run_test_yuv420_msssim():
+    """run_test(calc_ssim=True) on a YUV420 sequence: MS-SSIM of Y/U/V from
+    the GPU against the oracle's calc_msssim of the same recon planes."""
+    _need_gpu()
+    from dcvc_amd import hip as K
+    from dcvc_amd.harness import MsSsim, FrameStage
+    from dcvc_amd.synth import moving_pattern_yuv420
+    h, w = 200, 256
+    y, uv = moving_pattern_yuv420(h, w, 0, seed=9)
+    g = np.random.default_rng(9)
+    H, W = 208, 256
+    xh = torch.from_numpy((HO.yuv_u8_to_input(y, uv, H, W) + g.normal(0, 0.04, (H, W, 3))).astype(np.float32)).cuda()
+    act = K.Act(xh)
+    ms = MsSsim(h, w, 1, xh.device)
+    ms.run(act, torch.from_numpy(y).cuda(), torch.from_numpy(uv).cuda(), 0)
+    got = ms.values(1)[0]
+    crop = np.clip(xh.cpu().numpy()[:h, :w].transpose(2, 0, 1), 0, 1)
+    y_rec, uv_rec = HO.ycbcr444_to_420(np.ascontiguousarray(crop))
+    ref = [HO.calc_msssim(y.astype(np.float32) / 255, y_rec[0]),
+           HO.calc_msssim(uv[0].astype(np.float32) / 255, uv_rec[0]),
+           HO.calc_msssim(uv[1].astype(np.float32) / 255, uv_rec[1])]
+    np.testing.assert_allclose(got[:3], ref, rtol=0, atol=1e-10)
+    assert abs(got[3] - (6 * ref[0] + ref[1] + ref[2]) / 8) < 1e-10
