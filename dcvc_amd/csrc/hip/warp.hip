@@ -126,9 +126,48 @@ __device__ __forceinline__ float sigmoidf_(float v) { return 1.f / (1.f + expf(-
 
 // OffsetDiversity (video_model.py:43-63), one thread per (pixel, group g):
 // warps i = 2g, 2g+1 feed fusion group g (output channels 3g..3g+2).
-template <typename TF, typename TO, typename TY>
-__global__ void offset_div_kernel(View feat, View offs, View flow, View y, const float *fw,
-                                  const float *fb, const float *gx, const float *gy, float mag) {
+// Three consecutive bf16 channels c0..c0+2 at the four corners with two loads
+// per corner (a 4-byte pair and a 2-byte single) instead of three: the kernel
+// is bound by vector-memory instruction issue (SQ_WAIT_INST_ANY 0.75 of wave
+// cycles, profiles/r01_*), not by bytes.  ODD = parity of the element index of
+// c0 (uniform per call site); the interpolation order is sample()'s.
+template <int ODD>
+__device__ __forceinline__ void sample3_bf16(const View &x, const Bilin &b, int c0, float v[3]) {
+  const uint16_t *base = reinterpret_cast<const uint16_t *>(x.p) + x.co + c0;
+  const int64_t r0 = (int64_t)b.y0 * x.W, r1 = (int64_t)b.y1 * x.W;
+  const int64_t e[4] = {(r0 + b.x0) * x.cs, (r0 + b.x1) * x.cs, (r1 + b.x0) * x.cs, (r1 + b.x1) * x.cs};
+  float q[4][3];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const uint16_t *pp = base + e[k];
+    if constexpr (ODD == 0) {
+      const uint32_t pr = *reinterpret_cast<const uint32_t *>(pp);
+      q[k][0] = bf2f((uint16_t)(pr & 0xffffu));
+      q[k][1] = bf2f((uint16_t)(pr >> 16));
+      q[k][2] = bf2f(pp[2]);
+    } else {
+      const uint32_t pr = *reinterpret_cast<const uint32_t *>(pp + 1);
+      q[k][0] = bf2f(pp[0]);
+      q[k][1] = bf2f((uint16_t)(pr & 0xffffu));
+      q[k][2] = bf2f((uint16_t)(pr >> 16));
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < 3; ++c) v[c] = q[0][c] * b.nw + q[1][c] * b.ne + q[2][c] * b.sw + q[3][c] * b.se;
+}
+
+// PAIRED: bf16 features whose element offsets keep the parity of the channel
+// (even channel stride and offset, 4-byte aligned base): sample3_bf16.
+template <typename TF, typename TO, typename TY, bool PAIRED>
+__global__ void __launch_bounds__(256) offset_div_kernel(View feat, View offs, View flow, View y, const float *fw,
+                                                         const float *fb, const float *gx, const float *gy,
+                                                         float mag) {
+  // the grouped 1x1 fusion weights, read by every thread: LDS, not 21 more
+  // vector loads per thread
+  __shared__ float sfw[48 * 6], sfb[48];
+  for (int i = threadIdx.x; i < 48 * 6; i += 256) sfw[i] = fw[i];
+  if (threadIdx.x < 48) sfb[threadIdx.x] = fb[threadIdx.x];
+  __syncthreads();
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int g = (int)(t & 15);
   const int64_t pix = t >> 4;
@@ -181,16 +220,26 @@ __global__ void offset_div_kernel(View feat, View offs, View flow, View y, const
     const float msk = sigmoidf_(ov[4 + k]);
     const Bilin b = warp_coords(gx[px], gy[py], dx, dy, feat.W, feat.H);
     const int src_group = i & 15;                  // x.repeat(2,1,1,1)
+    if constexpr (PAIRED) {
+      float v3[3];
+      if (k == 0)
+        sample3_bf16<0>(feat, b, 3 * src_group, v3);  // src_group = 2g mod 16: even
+      else
+        sample3_bf16<1>(feat, b, 3 * src_group, v3);  // odd
 #pragma unroll
-    for (int c = 0; c < 3; ++c) xm[3 * k + c] = sample<TF>(feat, b, 3 * src_group + c) * msk;
+      for (int c = 0; c < 3; ++c) xm[3 * k + c] = v3[c] * msk;
+    } else {
+#pragma unroll
+      for (int c = 0; c < 3; ++c) xm[3 * k + c] = sample<TF>(feat, b, 3 * src_group + c) * msk;
+    }
   }
 #pragma unroll
   for (int c = 0; c < 3; ++c) {
     const int o = 3 * g + c;
     float acc = 0.f;
 #pragma unroll
-    for (int k = 0; k < 6; ++k) acc = acc + fw[o * 6 + k] * xm[k];
-    st<TY>(y.p, pix * y.cs + y.co + o, acc + fb[o]);
+    for (int k = 0; k < 6; ++k) acc = acc + sfw[o * 6 + k] * xm[k];
+    st<TY>(y.p, pix * y.cs + y.co + o, acc + sfb[o]);
   }
 }
 
@@ -307,14 +356,19 @@ extern "C" int dcvc_offset_diversity(dcvc_tensor feat, dcvc_tensor offs, dcvc_te
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const int64_t threads = (int64_t)y.H * y.W * 16;
   const unsigned grd = (unsigned)((threads + 255) / 256);
-#define LAUNCH(TF, TO, TY)                                                                  \
-  hipLaunchKernelGGL((offset_div_kernel<TF, TO, TY>), dim3(grd), dim3(256), 0, st, mk(feat), \
+#define LAUNCH(TF, TO, TY, PR)                                                                  \
+  hipLaunchKernelGGL((offset_div_kernel<TF, TO, TY, PR>), dim3(grd), dim3(256), 0, st, mk(feat), \
                      mk(offs), mk(flow), mk(y), fw, fb, gx, gy, max_mag)
   const bool f32 = feat.dtype == DCVC_F32, o32 = offs.dtype == DCVC_F32, y32 = y.dtype == DCVC_F32;
-  if (f32 && o32 && y32) LAUNCH(float, float, float);
-  else if (!f32 && !o32 && !y32) LAUNCH(uint16_t, uint16_t, uint16_t);
-  else if (!f32 && o32 && !y32) LAUNCH(uint16_t, float, uint16_t);
-  else return DCVC_HIP_EUNSUPPORTED;
+  const bool paired = !f32 && feat.cstride % 2 == 0 && feat.coff % 2 == 0 && ((uintptr_t)feat.ptr & 3) == 0;
+  if (f32 && o32 && y32) LAUNCH(float, float, float, false);
+  else if (!f32 && !o32 && !y32) {
+    if (paired) LAUNCH(uint16_t, uint16_t, uint16_t, true);
+    else LAUNCH(uint16_t, uint16_t, uint16_t, false);
+  } else if (!f32 && o32 && !y32) {
+    if (paired) LAUNCH(uint16_t, float, uint16_t, true);
+    else LAUNCH(uint16_t, float, uint16_t, false);
+  } else return DCVC_HIP_EUNSUPPORTED;
 #undef LAUNCH
   DCVC_LAUNCH_CHECK();
   return DCVC_HIP_OK;

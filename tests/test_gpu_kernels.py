@@ -559,3 +559,23 @@ def test_copy_and_pad_views(src_dt, dst_dt, coff, C, pad):
     got = dst.t().float().cpu()
     assert torch.equal(got[:, :, coff:coff + C].permute(2, 0, 1).unsqueeze(0), ref)
     assert not got[:, :, :coff].any() and not got[:, :, coff + C:].any()
+
+
+def test_offset_diversity_paired_bf16_loads_bit_identical():
+    """bf16 features: the paired-load path (even channel stride / offset) is
+    bit-identical to the per-channel path (odd offset view of a wider buffer)."""
+    h = K()
+    H, W = 40, 56
+    feat = torch.randn(1, 48, H, W)
+    flow = torch.randn(1, 2, H, W) * 3
+    offs = torch.randn(1, 96, H // 2, W // 2) * 0.05
+    fw = (torch.randn(48, 6) * 0.3).contiguous().cuda()
+    fb = (torch.randn(48) * 0.1).cuda()
+    fa = to_act(feat, h.BF16)                       # standalone 48-ch buffer: paired path
+    wide = h.zeros(H, W, 50, h.BF16)
+    h.copy(fa, wide.ch(1, 48))                      # coff 1: per-channel path
+    oa, fl = to_act(offs, h.F32), to_act(flow, h.F32)
+    y1 = h.offset_diversity(fa, oa, fl, fw, fb, _grid(H, W))
+    y2 = h.offset_diversity(wide.ch(1, 48), oa, fl, fw, fb, _grid(H, W))
+    torch.cuda.synchronize()
+    assert torch.equal(y1.t().cpu(), y2.t().cpu())
