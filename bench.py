@@ -422,6 +422,15 @@ def main():
         if tr:
             roof["traffic_source"] = tr["source"]
             roof["rocprof_avg_launch_us"] = tr["rocprof_avg_launch_us"]
+            # the PMC summary is keyed by instantiation@grid; a persistent
+            # kernel keeps its grid across layer shapes, so its per-launch
+            # average can mix layers.  Report traffic only when the rocprof
+            # average launch time agrees with this layer's (within 25 %).
+            ev = tsec / n * 1e6
+            if tr["rocprof_avg_launch_us"] and abs(tr["rocprof_avg_launch_us"] - ev) > 0.25 * ev:
+                roof["traffic"] = None
+                roof["traffic_note"] = ("PMC summary of this instantiation@grid averages several layer shapes "
+                                        f"(rocprof {tr['rocprof_avg_launch_us']} us vs {ev:.1f} us for this layer)")
         roof["kernel"] = kname
         roof["layer"] = shape
         roof["launches_per_P_frame"] = n

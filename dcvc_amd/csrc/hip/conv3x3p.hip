@@ -247,6 +247,44 @@ __global__ void __launch_bounds__(NW * 64) conv3p_kernel(P3 p) {
     const int tn = t + G;
     const bool more = tn < ntiles;
     if (more) issue(tn);  // in flight across this tile's MFMAs and epilogue
+    // epilogue-B plan and residual loads for this tile, issued before the
+    // MFMAs so their HBM latency hides behind them (pieces of 8 consecutive
+    // output channels of one output pixel, in output-row order; SHUF: conv
+    // channel n of pixel (y, x) is output channel n >> 2 of pixel
+    // (2y + (n >> 1 & 1), 2x + (n & 1)), pixel_shuffle(2))
+    int64_t ob[PO];
+    int src[PO], cq[PO];
+    bool ok[PO];
+    typename Vec8<TOUT>::raw r1[PO], r2[PO];
+    {
+      const int oy0 = (t / p.tiles_x) * TH, ox0 = (t % p.tiles_x) * 16;
+      constexpr int NQ = SHUF ? BN / 32 : BN / 8;  // pieces per (pixel, sub-position)
+#pragma unroll
+      for (int u = 0; u < PO; ++u) {
+        const int it = tid + u * NTHR;
+        const int q = it % NQ, r = it / NQ;
+        int l, oy, ox;
+        if constexpr (SHUF) {
+          const int dx = r & 1, cx = (r >> 1) & 15, dy = (r >> 5) & 1, cyl = r >> 6;
+          l = cyl * 16 + cx;
+          oy = 2 * (oy0 + cyl) + dy;
+          ox = 2 * (ox0 + cx) + dx;
+          ok[u] = it < TH * 16 * 4 * NQ && oy0 + cyl < p.H && ox0 + cx < p.W;
+          src[u] = l * LD + 4 * q * 8 + dy * 2 + dx;
+        } else {
+          l = r;
+          oy = oy0 + (l >> 4);
+          ox = ox0 + (l & 15);
+          ok[u] = it < TH * 16 * NQ && oy < p.H && ox < p.W;
+          src[u] = l * LD + q * 8;
+        }
+        cq[u] = q * 8;
+        ob[u] = (int64_t)oy * p.Wout + ox;
+        const int cb = (SHUF ? n0 / 4 : n0) + q * 8;
+        if (p.res) r1[u] = Vec8<TOUT>::load(rr, ok[u] ? (int)(ob[u] * p.rcs + p.rco + cb) : -1);
+        if (p.res2) r2[u] = Vec8<TOUT>::load(rr2, ok[u] ? (int)(ob[u] * p.r2cs + p.r2co + cb) : -1);
+      }
+    }
 
     f32x4 acc[RW][NT];
 #pragma unroll
@@ -313,41 +351,8 @@ __global__ void __launch_bounds__(NW * 64) conv3p_kernel(P3 p) {
     __syncthreads();
 
     // ---- epilogue B: out = scale * (res2 + (res + v)) in pieces of 8
-    // consecutive output channels of one output pixel, in output-row order
-    // (SHUF: conv channel n of pixel (y, x) is output channel n >> 2 of
-    // pixel (2y + (n >> 1 & 1), 2x + (n & 1)), pixel_shuffle(2))
+    // consecutive output channels (plan and residual loads issued above)
     {
-      const int oy0 = (t / p.tiles_x) * TH, ox0 = (t % p.tiles_x) * 16;
-      constexpr int NQ = SHUF ? BN / 32 : BN / 8;  // pieces per (pixel, sub-position)
-      int64_t ob[PO];
-      int src[PO], cq[PO];
-      bool ok[PO];
-      typename Vec8<TOUT>::raw r1[PO], r2[PO];
-#pragma unroll
-      for (int u = 0; u < PO; ++u) {
-        const int it = tid + u * NTHR;
-        const int q = it % NQ, r = it / NQ;
-        int l, oy, ox;
-        if constexpr (SHUF) {
-          const int dx = r & 1, cx = (r >> 1) & 15, dy = (r >> 5) & 1, cyl = r >> 6;
-          l = cyl * 16 + cx;
-          oy = 2 * (oy0 + cyl) + dy;
-          ox = 2 * (ox0 + cx) + dx;
-          ok[u] = it < TH * 16 * 4 * NQ && oy0 + cyl < p.H && ox0 + cx < p.W;
-          src[u] = l * LD + 4 * q * 8 + dy * 2 + dx;
-        } else {
-          l = r;
-          oy = oy0 + (l >> 4);
-          ox = ox0 + (l & 15);
-          ok[u] = it < TH * 16 * NQ && oy < p.H && ox < p.W;
-          src[u] = l * LD + q * 8;
-        }
-        cq[u] = q * 8;
-        ob[u] = (int64_t)oy * p.Wout + ox;
-        const int cb = (SHUF ? n0 / 4 : n0) + q * 8;
-        if (p.res) r1[u] = Vec8<TOUT>::load(rr, ok[u] ? (int)(ob[u] * p.rcs + p.rco + cb) : -1);
-        if (p.res2) r2[u] = Vec8<TOUT>::load(rr2, ok[u] ? (int)(ob[u] * p.r2cs + p.r2co + cb) : -1);
-      }
 #pragma unroll
       for (int u = 0; u < PO; ++u) {
         if (!ok[u]) continue;
