@@ -449,6 +449,17 @@ int pick_bn(const ConvP &p, hipStream_t st) {
       best_pad = pad;
     }
   }
+  // latent-resolution maps (68x120 at 1080p) give few spatial tiles even at
+  // TH = 4: split Cout into narrower n-tiles until the grid has >= 2 x 256
+  // workgroups (each output channel's sum is unchanged, so results are too)
+  {
+    const long tiles4 = (long)((p.Wo + 15) / 16) * ((p.Ho + 3) / 4);
+    while (best > 32 && tiles4 * ((p.cout + best - 1) / best) < 512) {
+      const int nb = best == 96 ? 48 : best / 2;
+      if ((p.cout + nb - 1) / nb * nb - p.cout > best_pad) break;  // no extra padding
+      best = nb;
+    }
+  }
   switch (best) {
     case 16: return pick_th<TIN, TOUT, F32, 16>(p, st);
     case 32: return pick_th<TIN, TOUT, F32, 32>(p, st);
