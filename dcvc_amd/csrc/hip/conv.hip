@@ -512,6 +512,7 @@ extern "C" void dcvc_internal_conv3x3_resident(int v);
 extern "C" void dcvc_internal_conv3p_enable(int v);
 extern "C" void dcvc_internal_dcbp_enable(int v);
 extern "C" void dcvc_internal_conv3p_occupancy(int v);
+extern "C" void dcvc_internal_gemm1x1_bm(int v);
 
 extern "C" int dcvc_conv2d(const dcvc_conv_args *a, void *stream) {
   if (!a || !a->w || !valid_view(a->x) || !valid_view(a->y)) return DCVC_HIP_EINVAL;
@@ -614,6 +615,10 @@ extern "C" int dcvc_set_option(const char *name, int value) {
   }
   if (std::strcmp(name, "conv3x3_resident") == 0) {
     dcvc_internal_conv3x3_resident(value);
+    return DCVC_HIP_OK;
+  }
+  if (std::strcmp(name, "gemm1x1_bm") == 0) {
+    dcvc_internal_gemm1x1_bm(value);
     return DCVC_HIP_OK;
   }
   if (std::strcmp(name, "conv3x3_occupancy") == 0) {

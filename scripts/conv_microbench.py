@@ -29,6 +29,8 @@ SHAPES = [
     (7, 1, 32, 64, 1088, 1920),
     (1, 1, 384, 384, 68, 120),
     (1, 1, 48, 48, 1088, 1920),
+    (1, 1, 64, 64, 1088, 1920),
+    (1, 1, 64, 32, 1088, 1920),
 ]
 
 
