@@ -6,7 +6,7 @@ squeeze-excitation layer, the HEM UNet and the enc/dec towers."""
 import torch
 
 from .. import hip as K
-from ..hip import F32, ACT_LRELU, ACT_NONE, IN_LRELU, IN_NONE
+from ..hip import F32, BF16, ACT_LRELU, ACT_NONE, IN_LRELU, IN_NONE
 from ..layers import ResidualBlockWithStride, ResidualBlockUpsample
 
 
@@ -136,8 +136,14 @@ class Seq3:
         self.c4 = ctx.conv(p + ".4", latent=True, out_perm=out_perm)
 
     def __call__(self, x, y=None):
-        x = K.conv(self.c0, x, out_dtype=F32, act=ACT_LRELU, slope=0.2)
-        x = K.conv(self.c2, x, out_dtype=F32, act=ACT_LRELU, slope=0.2)
+        # the two intermediate maps feed only the next conv: with bf16 compute
+        # that conv rounds its input to bf16 on staging, so storing them as
+        # bf16 (the epilogue's identical RNE rounding) changes no value and
+        # halves their traffic; parity mode (f32 compute) keeps fp32
+        mid0 = BF16 if self.c2.compute == BF16 else F32
+        mid1 = BF16 if self.c4.compute == BF16 else F32
+        x = K.conv(self.c0, x, out_dtype=mid0, act=ACT_LRELU, slope=0.2)
+        x = K.conv(self.c2, x, out_dtype=mid1, act=ACT_LRELU, slope=0.2)
         return K.conv(self.c4, x, y, out_dtype=F32)
 
 

@@ -152,8 +152,13 @@ class DepthConvBlock:
         if self.gated:
             h = K.conv(self.ffn1, dc)
             return K.conv(self.ffn2, h, y, in_op=IN_GATE, in_slope=self.slope_ffn, res=dc, scale=scale)
-        h = K.conv(self.ffn1, dc, act=ACT_LRELU, slope=self.slope_ffn)
-        return K.conv(self.ffn2, h, y, act=ACT_LRELU, slope=self.slope_ffn, res=dc, scale=scale)
+        # the hidden layer feeds only ffn2: with bf16 compute ffn2 rounds it
+        # to bf16 on staging anyway, so it is stored as bf16 (same values,
+        # half the traffic of the 4x-wide map)
+        hid = BF16 if self.ffn2.compute == BF16 else dt
+        h = K.conv(self.ffn1, dc, out_dtype=hid, act=ACT_LRELU, slope=self.slope_ffn)
+        return K.conv(self.ffn2, h, y, out_dtype=dc.dtype, act=ACT_LRELU, slope=self.slope_ffn, res=dc,
+                      scale=scale)
 
 
 class ResidualBlockWithStride:

@@ -31,6 +31,10 @@ SHAPES = [
     (1, 1, 48, 48, 1088, 1920),
     (1, 1, 64, 64, 1088, 1920),
     (1, 1, 64, 32, 1088, 1920),
+    (3, 1, 480, 384, 68, 120),
+    (3, 1, 384, 288, 68, 120),
+    (3, 1, 288, 288, 68, 120),
+    (3, 1, 192, 192, 68, 120),
 ]
 
 
