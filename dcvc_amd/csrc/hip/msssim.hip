@@ -189,3 +189,70 @@ extern "C" int dcvc_down2_f64(const double *in, int h, int w, double *out, void 
   DCVC_LAUNCH_CHECK();
   return DCVC_HIP_OK;
 }
+
+// ---- RGB MS-SSIM (pytorch_msssim.ms_ssim as DCVC-DC/test_video.py:188 and
+// DCVC-HEM/test_video.py:153 call it; the package is not installed here, so
+// this follows its published algorithm: same Gaussian statistics per level,
+// downsampling by F.avg_pool2d(kernel 2, padding = size % 2,
+// count_include_pad=True), relu on cs / ssim).
+namespace {
+
+__global__ void rgb_planes_kernel(const float *xh, int xW, int xcs, int xco, const uint8_t *src, int h, int w,
+                                  double *sp, double *rp) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t n = (int64_t)h * w;
+  if (i >= n) return;
+  const int y = (int)(i / w), x = (int)(i - (int64_t)y * w);
+  const float *p = xh + ((int64_t)y * xW + x) * xcs + xco;
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    sp[c * n + i] = (double)((float)src[c * n + i] / 255.f);
+    rp[c * n + i] = (double)fminf(fmaxf(p[c], 0.f), 1.f);
+  }
+}
+
+// F.avg_pool2d(kernel_size=2, stride=2, padding=(h % 2, w % 2)),
+// count_include_pad=True: output (h + 2 ph - 2) / 2 + 1 rows; window i covers
+// input rows 2i - ph, 2i - ph + 1 (zeros outside), always divided by 4
+__global__ void avgpool2_kernel(const double *in, int h, int w, double *out) {
+  const int ph = h & 1, pw = w & 1;
+  const int oh = (h + 2 * ph - 2) / 2 + 1, ow = (w + 2 * pw - 2) / 2 + 1;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)oh * ow) return;
+  const int oy = (int)(i / ow), ox = (int)(i - (int64_t)oy * ow);
+  double s = 0.0;
+#pragma unroll
+  for (int dy = 0; dy < 2; ++dy)
+#pragma unroll
+    for (int dx = 0; dx < 2; ++dx) {
+      const int y = 2 * oy - ph + dy, x = 2 * ox - pw + dx;
+      if (y >= 0 && y < h && x >= 0 && x < w) s += in[(int64_t)y * w + x];
+    }
+  out[i] = s / 4.0;
+}
+
+}  // namespace
+
+extern "C" int dcvc_rgb_planes_f64(dcvc_tensor x_hat, const uint8_t *src, int h, int w, double *src_planes,
+                                   double *rec_planes, void *stream) {
+  if (!x_hat.ptr || x_hat.dtype != DCVC_F32 || x_hat.C != 3 || x_hat.H < h || x_hat.W < w || !src ||
+      !src_planes || !rec_planes || h < 1 || w < 1)
+    return DCVC_HIP_EINVAL;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int64_t n = (int64_t)h * w;
+  hipLaunchKernelGGL(rgb_planes_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st,
+                     reinterpret_cast<const float *>(x_hat.ptr), x_hat.W, x_hat.cstride, x_hat.coff, src, h, w,
+                     src_planes, rec_planes);
+  DCVC_LAUNCH_CHECK();
+  return DCVC_HIP_OK;
+}
+
+extern "C" int dcvc_avgpool2_f64(const double *in, int h, int w, double *out, void *stream) {
+  if (!in || !out || h < 2 || w < 2) return DCVC_HIP_EINVAL;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int oh = (h + 2 * (h & 1) - 2) / 2 + 1, ow = (w + 2 * (w & 1) - 2) / 2 + 1;
+  const int64_t n = (int64_t)oh * ow;
+  hipLaunchKernelGGL(avgpool2_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, in, h, w, out);
+  DCVC_LAUNCH_CHECK();
+  return DCVC_HIP_OK;
+}

@@ -13,9 +13,10 @@ PSNR formulas are evaluated on the host exactly as the reference writes them.
 
 MS-SSIM: for YUV420 sources ``calc_ssim`` runs the reference's per-plane
 ``calc_msssim`` (src/utils/metrics.py:39-62) on the GPU in fp64 (``MsSsim``,
-msssim.hip).  RGB MS-SSIM is ``pytorch_msssim.ms_ssim`` in the reference (DC
-and HEM), a package absent from this image, so it cannot be pinned: it is
-reported as 0 with ``msssim_unavailable`` set in the log.
+msssim.hip), pinned to the reference's outputs.  RGB MS-SSIM is
+``pytorch_msssim.ms_ssim`` in the reference (DC and HEM), a package absent
+from this image: ``MsSsimRGB`` follows its published algorithm on the GPU and
+the log carries ``msssim_unpinned``.
 """
 import os
 import time
@@ -230,6 +231,59 @@ class MsSsim:
         return res
 
 
+class MsSsimRGB:
+    """pytorch_msssim.ms_ssim(x_hat, x, data_range=1) as DCVC-DC/test_video.py:188
+    and DCVC-HEM/test_video.py:153 call it, on the GPU in fp64.  The package is
+    not installed here, so this follows its published algorithm (5 levels,
+    weights W5, Gaussian 11 / 1.5 'valid' statistics (dcvc_ssim_level), relu on
+    cs and ssim, F.avg_pool2d(2, padding=size % 2) between levels
+    (dcvc_avgpool2_f64), mean over the 3 channels); parity unpinned."""
+
+    def __init__(self, h, w, frame_num, device):
+        if min(h, w) <= 160:
+            raise ValueError("ms_ssim needs the smaller side > (11 - 1) * 2**4")
+        self.h, self.w = h, w
+        n = 3 * h * w
+        self.src = torch.empty(n, dtype=torch.float64, device=device)
+        self.rec = torch.empty(n, dtype=torch.float64, device=device)
+        x = np.arange(11, dtype=np.float64) - 5
+        g = np.exp(-(x ** 2) / (2 * 1.5 ** 2))
+        g /= g.sum()
+        self.win = torch.from_numpy(np.outer(g, g)).to(device)
+        self.ws = torch.empty(int(K.lib().dcvc_ssim_workspace()) // 8, dtype=torch.float64, device=device)
+        self.out = torch.zeros((max(frame_num, 1), 3, 5, 2), dtype=torch.float64, device=device)
+        self.bufs, sh, sw = [], h, w
+        for _ in range(4):
+            sh, sw = (sh + 2 * (sh % 2) - 2) // 2 + 1, (sw + 2 * (sw % 2) - 2) // 2 + 1
+            self.bufs.append([torch.empty(sh * sw, dtype=torch.float64, device=device) for _ in range(6)] + [sh, sw])
+
+    def run(self, x_hat, src_u8, slot):
+        K.rgb_planes_f64(x_hat, src_u8, self.h, self.w, self.src, self.rec)
+        n = self.h * self.w
+        for c in range(3):
+            a, b, sh, sw = self.src[c * n:(c + 1) * n], self.rec[c * n:(c + 1) * n], self.h, self.w
+            for k in range(5):
+                K.ssim_level(a, b, sh, sw, self.win, self.ws, self.out[slot, c, k])
+                if k < 4:
+                    bufs = self.bufs[k]
+                    na, nb, nh, nw = bufs[2 * c], bufs[2 * c + 1], bufs[6], bufs[7]
+                    K.avgpool2_f64(a, sh, sw, na)
+                    K.avgpool2_f64(b, sh, sw, nb)
+                    a, b, sh, sw = na, nb, nh, nw
+
+    def values(self, n):
+        o = self.out[:n].cpu().numpy()
+        res = []
+        for f in range(n):
+            per = []
+            for c in range(3):
+                mcs = np.maximum(o[f, c, :4, 1], 0.0)
+                ssim = max(o[f, c, 4, 0], 0.0)
+                per.append(float(np.prod(np.append(mcs, ssim) ** MsSsim.W5)))
+            res.append(float(np.mean(per)))
+        return res
+
+
 def psnr_rgb(sse3, h, w):
     """PSNR() of test_video.py:65-68: mse = mean((x_hat - x)^2) as an fp32
     tensor, psnr = 20 * log10(1 / sqrt(mse)) in fp32."""
@@ -348,7 +402,9 @@ def run_test(p_frame_net, i_frame_net, args):
     reader = _reader(args, yuv)
     h, w = args["src_height"], args["src_width"]
     stage = FrameStage(h, w, 16, yuv, zero_pad=False, frame_num=frame_num, device=device)
-    ms = MsSsim(h, w, frame_num, device) if (yuv and args.get("calc_ssim")) else None
+    ms = None
+    if args.get("calc_ssim"):
+        ms = MsSsim(h, w, frame_num, device) if yuv else MsSsimRGB(h, w, frame_num, device)
     frame_types, bits = [], []
     start_time = time.time()
     p_frame_number = 0
@@ -383,7 +439,10 @@ def run_test(p_frame_net, i_frame_net, args):
             stage.distortion(recon, dframe, frame_idx)
             if ms is not None:
                 from .dc.video_model import as_act
-                ms.run(as_act(recon), dframe[0], dframe[1], frame_idx)
+                if yuv:
+                    ms.run(as_act(recon), dframe[0], dframe[1], frame_idx)
+                else:
+                    ms.run(as_act(recon), dframe, frame_idx)
             if verbose >= 2:
                 print(f"frame {frame_idx}, bits: {bits[-1]:.3f}", flush=True)
     sse = stage.sums()
@@ -401,10 +460,11 @@ def run_test(p_frame_net, i_frame_net, args):
                                 [m[0] for m in mv], [m[1] for m in mv], [m[2] for m in mv], verbose=verbose >= 1)
     else:
         psnrs = [psnr_rgb(sse[i], h, w) for i in range(frame_num)]
-        log = generate_log_json(frame_num, h * w, test_time, frame_types, bits, psnrs, zeros,
+        mv = ms.values(frame_num) if ms is not None else zeros
+        log = generate_log_json(frame_num, h * w, test_time, frame_types, bits, psnrs, mv,
                                 verbose=verbose >= 1)
     if args.get("calc_ssim") and not yuv:
-        log["msssim_unavailable"] = True
+        log["msssim_unpinned"] = True   # pytorch_msssim's algorithm, package absent (MsSsimRGB)
     return log
 
 
@@ -430,6 +490,7 @@ def run_test_hem(video_net, i_frame_net, args, device=None):
     reader = _reader({**args, "src_type": args.get("src_type", "png")}, False)
     h, w = args["src_height"], args["src_width"]
     stage = FrameStage(h, w, 64, False, zero_pad=True, frame_num=frame_num, device=device)
+    ms = MsSsimRGB(h, w, frame_num, device) if min(h, w) > 160 else None  # HEM always reports ms_ssim (:150)
     frame_types, bits = [], []
     start_time = time.time()
     dpb = None
@@ -455,9 +516,12 @@ def run_test_hem(video_net, i_frame_net, args, device=None):
                 frame_types.append(1)
             bits.append(result["bit"])
             stage.distortion(recon, dframe, frame_idx)
+            if ms is not None:
+                from .dc.video_model import as_act
+                ms.run(as_act(recon), dframe, frame_idx)
     sse = stage.sums()
     psnrs = [psnr_rgb(sse[i], h, w) for i in range(frame_num)]
-    log = generate_log_json_hem(frame_num, frame_types, bits, psnrs, [0.0] * frame_num, h * w,
-                                time.time() - start_time)
-    log["msssim_unavailable"] = True
+    mv = ms.values(frame_num) if ms is not None else [0.0] * frame_num
+    log = generate_log_json_hem(frame_num, frame_types, bits, psnrs, mv, h * w, time.time() - start_time)
+    log["msssim_unpinned"] = True   # pytorch_msssim's algorithm, package absent (MsSsimRGB)
     return log

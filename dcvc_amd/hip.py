@@ -91,6 +91,8 @@ HIP_SYMBOLS = [
     ("dcvc_ssim_workspace", ctypes.c_int64, []),
     ("dcvc_ssim_level", _i, [_vp, _vp, _i, _i, _vp, ctypes.c_double, ctypes.c_double, _vp, _vp, _vp]),
     ("dcvc_down2_f64", _i, [_vp, _i, _i, _vp, _vp]),
+    ("dcvc_rgb_planes_f64", _i, [_T, _vp, _i, _i, _vp, _vp, _vp]),
+    ("dcvc_avgpool2_f64", _i, [_vp, _i, _i, _vp, _vp]),
     ("dcvc_debug_poison_lds", _i, [_i, _i, _vp]),
     ("dcvc_debug_poison_vgpr", _i, [_i, _vp]),
 ]
@@ -489,6 +491,16 @@ def ssim_level(a, b, h, w, window, workspace, out2):
     """Means of calc_ssim's ssim and cs maps of two fp64 h x w planes."""
     check(lib().dcvc_ssim_level(a.data_ptr(), b.data_ptr(), h, w, window.data_ptr(), 1e-4, 9e-4,
                                 workspace.data_ptr(), out2.data_ptr(), stream()), "ssim_level")
+
+
+def rgb_planes_f64(x_hat, src_u8, h, w, src, rec):
+    assert src.numel() >= 3 * h * w and rec.numel() >= 3 * h * w
+    check(lib().dcvc_rgb_planes_f64(x_hat.c(), src_u8.data_ptr(), h, w, src.data_ptr(), rec.data_ptr(), stream()),
+          "rgb_planes_f64")
+
+
+def avgpool2_f64(x, h, w, y):
+    check(lib().dcvc_avgpool2_f64(x.data_ptr(), h, w, y.data_ptr(), stream()), "avgpool2_f64")
 
 
 def down2_f64(x, h, w, y):

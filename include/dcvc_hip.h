@@ -317,6 +317,16 @@ int dcvc_ssim_level(const double *a, const double *b, int h, int w,
                     const double *window121, double C1, double C2,
                     double *workspace, double *out2, void *stream);
 int dcvc_down2_f64(const double *in, int h, int w, double *out, void *stream);
+/* RGB MS-SSIM (pytorch_msssim.ms_ssim, DCVC-DC/test_video.py:188,
+ * DCVC-HEM/test_video.py:153; the package is absent here, so its published
+ * algorithm is followed and the result is parity unpinned).
+ * dcvc_rgb_planes_f64: the three fp64 source (uint8/255) and clamped recon
+ * planes of the h x w crop; levels use dcvc_ssim_level and
+ * dcvc_avgpool2_f64 = F.avg_pool2d(kernel 2, padding h%2 / w%2,
+ * count_include_pad=True) (out: (h + 2(h%2) - 2)/2 + 1 rows). */
+int dcvc_rgb_planes_f64(dcvc_tensor x_hat, const uint8_t *src, int h, int w,
+                        double *src_planes, double *rec_planes, void *stream);
+int dcvc_avgpool2_f64(const double *in, int h, int w, double *out, void *stream);
 
 /* Debug aid: fill the LDS of `blocks` workgroups with all-ones bytes (NaN in
  * bf16 / fp32), to expose kernels that read LDS they never wrote

@@ -154,3 +154,41 @@ def calc_msssim(img1, img2, data_range=1.0):
         im1, im2 = down2_reflect(im1), down2_reflect(im2)
     mssim, mcs = np.array(mssim), np.array(mcs)
     return np.prod(mcs[0:level - 1] ** weight[0:level - 1]) * (mssim[level - 1] ** weight[level - 1])
+
+
+def ms_ssim_torch(X, Y, data_range=1.0):
+    """pytorch_msssim.ms_ssim (size_average=True, win 11 / 1.5, K (0.01, 0.03),
+    default weights) restated from its published algorithm in fp32 torch —
+    the package is not installed, so this restatement is parity unpinned.
+    X, Y: (N, C, H, W) float tensors."""
+    import torch.nn.functional as F
+    coords = torch.arange(11, dtype=torch.float) - 5
+    g = torch.exp(-(coords ** 2) / (2 * 1.5 ** 2))
+    g = (g / g.sum()).reshape(1, 1, 1, 11)
+    C = X.shape[1]
+    wh, wv = g.repeat(C, 1, 1, 1), g.transpose(2, 3).repeat(C, 1, 1, 1)
+
+    def filt(x):
+        return F.conv2d(F.conv2d(x, wv, groups=C), wh, groups=C)
+
+    def ssim(x, y):
+        C1, C2 = (0.01 * data_range) ** 2, (0.03 * data_range) ** 2
+        mu1, mu2 = filt(x), filt(y)
+        m1s, m2s, m12 = mu1.pow(2), mu2.pow(2), mu1 * mu2
+        s1, s2, s12 = filt(x * x) - m1s, filt(y * y) - m2s, filt(x * y) - m12
+        cs_map = (2 * s12 + C2) / (s1 + s2 + C2)
+        ssim_map = ((2 * m12 + C1) / (m1s + m2s + C1)) * cs_map
+        return torch.flatten(ssim_map, 2).mean(-1), torch.flatten(cs_map, 2).mean(-1)
+
+    weights = torch.tensor([0.0448, 0.2856, 0.3001, 0.2363, 0.1333])
+    mcs = []
+    for i in range(5):
+        s, cs = ssim(X, Y)
+        if i < 4:
+            mcs.append(torch.relu(cs))
+            pad = [d % 2 for d in X.shape[2:]]
+            X = F.avg_pool2d(X, kernel_size=2, padding=pad)
+            Y = F.avg_pool2d(Y, kernel_size=2, padding=pad)
+    s = torch.relu(s)
+    v = torch.prod(torch.stack(mcs + [s], dim=0) ** weights.view(-1, 1, 1), dim=0)
+    return v.mean().item()

@@ -324,3 +324,33 @@ def test_run_test_yuv420_msssim():
            HO.calc_msssim(uv[1].astype(np.float32) / 255, uv_rec[1])]
     np.testing.assert_allclose(got[:3], ref, rtol=0, atol=1e-10)
     assert abs(got[3] - (6 * ref[0] + ref[1] + ref[2]) / 8) < 1e-10
+
+
+def test_avgpool2_padding_semantics():
+    """avg_pool2d(kernel 2, padding = size % 2, count_include_pad) as the
+    GPU kernel restates it: zero rows/columns on both sides of odd sizes."""
+    import torch.nn.functional as F
+    x = torch.arange(35, dtype=torch.float64).reshape(1, 1, 5, 7)
+    got = F.avg_pool2d(x, kernel_size=2, padding=[1, 1])
+    p = F.pad(x, (1, 1, 1, 1))
+    ref = (p[..., 0:-1:2, 0:-1:2] + p[..., 0:-1:2, 1::2] + p[..., 1::2, 0:-1:2] + p[..., 1::2, 1::2]) / 4
+    assert torch.equal(got, ref[..., :got.shape[2], :got.shape[3]])
+
+
+@gpu
+@pytest.mark.parametrize("h,w", [(256, 256), (181, 243), (1080, 1920)])
+def test_gpu_rgb_msssim_matches_restatement(h, w):
+    """MsSsimRGB (fp64 GPU) vs the fp32 torch restatement of pytorch_msssim
+    (parity unpinned: the package is absent); agreement to 1e-5."""
+    _need_gpu()
+    from dcvc_amd import hip as K
+    from dcvc_amd.harness import MsSsimRGB
+    g = np.random.default_rng(h)
+    src = g.integers(0, 256, (3, h, w), dtype=np.uint8)
+    rec = np.clip(src.astype(np.float32) / 255 + g.normal(0, 0.05, (3, h, w)).astype(np.float32), 0, 1)
+    xh = torch.from_numpy(np.ascontiguousarray(rec.transpose(1, 2, 0))).cuda()
+    ms = MsSsimRGB(h, w, 1, xh.device)
+    ms.run(K.Act(xh), torch.from_numpy(src).cuda(), 0)
+    got = ms.values(1)[0]
+    ref = HO.ms_ssim_torch(torch.from_numpy(rec)[None], torch.from_numpy(src.astype(np.float32) / 255)[None])
+    assert abs(got - ref) < 1e-5, (got, ref)
