@@ -420,12 +420,16 @@ int launch(const ConvP &p0, hipStream_t st) {
 // Tile choice: BN covers Cout in the fewest n-tiles (max 128); TH shrinks
 // from 16 (8 when strided) to 4 until the grid has >= 1024 workgroups, so
 // the small latent-resolution GEMMs still fill the 256 CUs.
+int g_force_th = 0;  // dcvc_set_option("conv_th", 4 | 8 | 16): A/B of the tile height (7x7 convs)
+int g_force_bn = 0;  // dcvc_set_option("conv_bn", 16..128): A/B of the n-tile width (7x7 convs)
+
 template <typename TIN, typename TOUT, bool F32, int BN>
 int pick_th(const ConvP &p, hipStream_t st) {
   const int64_t tx = (p.Wo + 15) / 16, tn = (p.cout + BN - 1) / BN;
   auto blocks = [&](int th) { return tx * ((p.Ho + th - 1) / th) * tn; };
   int th = (p.s > 1 || BN > 64) ? 8 : 16;
   while (th > 4 && blocks(th) < 1024) th /= 2;
+  if (g_force_th && p.kh == 7) th = g_force_th;
   if (th == 16 && BN <= 64 && lds_bytes<F32, BN, 16>(p, false) <= 160 * 1024)
     return launch<TIN, TOUT, F32, BN, 16>(p, st);
   if (th >= 8) return launch<TIN, TOUT, F32, BN, 8>(p, st);
@@ -460,6 +464,7 @@ int pick_bn(const ConvP &p, hipStream_t st) {
       best = nb;
     }
   }
+  if (g_force_bn && p.kh == 7) best = g_force_bn;
   switch (best) {
     case 16: return pick_th<TIN, TOUT, F32, 16>(p, st);
     case 32: return pick_th<TIN, TOUT, F32, 32>(p, st);
@@ -615,6 +620,14 @@ extern "C" int dcvc_set_option(const char *name, int value) {
   }
   if (std::strcmp(name, "conv3x3_resident") == 0) {
     dcvc_internal_conv3x3_resident(value);
+    return DCVC_HIP_OK;
+  }
+  if (std::strcmp(name, "conv_th") == 0) {
+    g_force_th = value;
+    return DCVC_HIP_OK;
+  }
+  if (std::strcmp(name, "conv_bn") == 0) {
+    g_force_bn = value;
     return DCVC_HIP_OK;
   }
   if (std::strcmp(name, "gemm1x1_bm") == 0) {

@@ -27,6 +27,9 @@ SHAPES = [
     (3, 1, 128, 128, 68, 120),
     (3, 2, 48, 64, 1088, 1920),
     (7, 1, 32, 64, 1088, 1920),
+    (7, 1, 64, 32, 1088, 1920),
+    (7, 1, 8, 32, 1088, 1920),
+    (7, 1, 32, 16, 1088, 1920),
     (1, 1, 384, 384, 68, 120),
     (1, 1, 48, 48, 1088, 1920),
     (1, 1, 64, 64, 1088, 1920),
