@@ -21,8 +21,8 @@ n = int(sys.argv[1]) if len(sys.argv) > 1 else 6
 dev = torch.device("cuda", 0)
 isd, psd = bench.make_weights(None, 0, dev)
 prec = Precision.fast(latent_compute=K.BF16)
-inet = IntraNoAR(precision=prec, device=dev).load_state_dict(isd)
-pnet = DMC(precision=prec, device=dev).load_state_dict(psd)
+inet = IntraNoAR(precision=prec, stream_part=8, device=dev).load_state_dict(isd)
+pnet = DMC(precision=prec, stream_part=8, device=dev).load_state_dict(psd)
 inet.update(force=True)
 pnet.update(force=True)
 h, w = 1080, 1920
