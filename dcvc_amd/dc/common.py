@@ -41,8 +41,8 @@ class SymbolBuffer:
     def to_host(self):
         s = K.pinned("sb_sym", self.sym.numel(), self.sym_dtype)
         x = K.pinned("sb_idx", self.idx.numel(), torch.int16)
-        s.copy_(self.sym, non_blocking=True)
-        x.copy_(self.idx, non_blocking=True)
+        s.copy_(self.sym, non_blocking=K.ASYNC_COPIES)
+        x.copy_(self.idx, non_blocking=K.ASYNC_COPIES)
         torch.cuda.current_stream().synchronize()
         s, x = s.numpy(), x.numpy()
         return [(s[self.offs[i]:self.offs[i + 1]], x[self.offs[i]:self.offs[i + 1]]) for i in range(len(self.sizes))]
@@ -111,10 +111,10 @@ class QuadtreePrior:
         for k in range(4):
             sm = None if k == 0 else self.step_params(buf, k)
             K.qt_indexes_step(params, sm, k, idx_d, scale_table.log_min, scale_table.log_step)
-            idx_h.copy_(idx_d, non_blocking=True)
+            idx_h.copy_(idx_d, non_blocking=K.ASYNC_COPIES)
             torch.cuda.current_stream().synchronize()
             sym_h.numpy()[:] = decode_fn(idx_h.numpy())
-            sym_d.copy_(sym_h, non_blocking=True)
+            sym_d.copy_(sym_h, non_blocking=K.ASYNC_COPIES)
             K.qt_decode_step(params, sm, k, sym_d, buf.ch(0, C), yhat)
         return yhat
 

@@ -58,10 +58,10 @@ class DualPrior:
         for k in range(2):
             sm = None if k == 0 else self.spatial(buf)
             K.dp_indexes_step(buf, sm, k, idx_d, scale_table.log_min, scale_table.log_step)
-            idx_h.copy_(idx_d, non_blocking=True)
+            idx_h.copy_(idx_d, non_blocking=K.ASYNC_COPIES)
             torch.cuda.current_stream().synchronize()
             sym_h.numpy()[:] = decode_fn(idx_h.numpy())
-            sym_d.copy_(sym_h, non_blocking=True)
+            sym_d.copy_(sym_h, non_blocking=K.ASYNC_COPIES)
             K.dp_decode_step(buf, sm, k, sym_d, yhat, post)
         return yhat
 

@@ -6,6 +6,7 @@ the allocator and the stream provider; every computation below is one of our
 kernels.  Calls are asynchronous on the current HIP stream.
 """
 import ctypes
+import os
 import threading
 
 import numpy as np
@@ -141,6 +142,10 @@ _get_device = getattr(torch._C, "_cuda_getDevice", None)
 
 _tls = threading.local()
 
+# Experiment switch (DCVC_BLOCKING_COPIES=1): host<->device symbol / index
+# transfers as blocking copies instead of async copies on the stream.
+ASYNC_COPIES = os.environ.get("DCVC_BLOCKING_COPIES", "0") != "1"
+
 
 def pinned(key, n, dtype):
     """Persistent pinned host staging buffer of this host thread (first n
@@ -177,7 +182,7 @@ def upload(arr, device, key):
     src = pinned(("upload", key), arr.size, dt)
     src.numpy()[:] = arr.reshape(-1)
     out = torch.empty(arr.shape, dtype=dt, device=device)
-    out.view(-1).copy_(src, non_blocking=True)
+    out.view(-1).copy_(src, non_blocking=ASYNC_COPIES)
     e = torch.cuda.Event()
     e.record()
     d[key] = e
