@@ -77,13 +77,20 @@ __global__ void warp_kernel(View x, View f, View y, const float *gx, const float
     st<TY>(y.p, pix * y.cs + y.co + c, sample<TX>(x, b, c));
 }
 
+// Workgroups are dealt to the 8 XCDs round robin; with a grid padded to a
+// multiple of 8, this bijection gives each XCD one contiguous band of the
+// frame, so the bilinear gathers of neighbouring pixels share that XCD's L2.
+__device__ __forceinline__ int64_t xcd_band(unsigned b, unsigned nb) {
+  return (int64_t)(b & 7u) * (nb >> 3) + (b >> 3);
+}
+
 // Vector form for bf16 maps with 8-channel-aligned views: one thread per
 // (pixel, 8 channels), 16-byte corner loads and one 16-byte store instead of
 // 32 two-byte loads (the scalar kernel is load-instruction bound).  Same
 // per-channel arithmetic, so results are identical.
 __global__ void warp8_kernel(View x, View f, View y, const float *gx, const float *gy) {
   const int q8 = y.C >> 3;
-  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t t = xcd_band(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
   const int64_t pix = t / q8;
   if (pix >= (int64_t)y.H * y.W) return;
   const int c = (int)(t - pix * q8) * 8;
@@ -126,30 +133,31 @@ __device__ __forceinline__ float sigmoidf_(float v) { return 1.f / (1.f + expf(-
 
 // OffsetDiversity (video_model.py:43-63), one thread per (pixel, group g):
 // warps i = 2g, 2g+1 feed fusion group g (output channels 3g..3g+2).
-// Three consecutive bf16 channels c0..c0+2 at the four corners with two loads
-// per corner (a 4-byte pair and a 2-byte single) instead of three: the kernel
-// is bound by vector-memory instruction issue (SQ_WAIT_INST_ANY 0.75 of wave
-// cycles, profiles/r01_*), not by bytes.  ODD = parity of the element index of
-// c0 (uniform per call site); the interpolation order is sample()'s.
+// Three consecutive bf16 channels c0..c0+2 at the four corners with ONE
+// 8-byte load per corner: the dword-aligned 4-channel window starting at c0
+// (ODD == 0) or c0 - 1 (ODD == 1) holds all three.  The kernel is bound by
+// vector-memory instruction issue on these gathers (SQ_WAIT_INST_ANY 0.75 of
+// wave cycles, profiles/r01_*), not by bytes.  ODD = parity of the element
+// index of c0 (uniform per call site); the interpolation order is sample()'s.
+struct __attribute__((aligned(4))) u32x2a4 { uint32_t lo, hi; };
+
 template <int ODD>
 __device__ __forceinline__ void sample3_bf16(const View &x, const Bilin &b, int c0, float v[3]) {
-  const uint16_t *base = reinterpret_cast<const uint16_t *>(x.p) + x.co + c0;
+  const uint16_t *base = reinterpret_cast<const uint16_t *>(x.p) + x.co + c0 - ODD;
   const int64_t r0 = (int64_t)b.y0 * x.W, r1 = (int64_t)b.y1 * x.W;
   const int64_t e[4] = {(r0 + b.x0) * x.cs, (r0 + b.x1) * x.cs, (r1 + b.x0) * x.cs, (r1 + b.x1) * x.cs};
   float q[4][3];
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
-    const uint16_t *pp = base + e[k];
+    const u32x2a4 w = *reinterpret_cast<const u32x2a4 *>(base + e[k]);
     if constexpr (ODD == 0) {
-      const uint32_t pr = *reinterpret_cast<const uint32_t *>(pp);
-      q[k][0] = bf2f((uint16_t)(pr & 0xffffu));
-      q[k][1] = bf2f((uint16_t)(pr >> 16));
-      q[k][2] = bf2f(pp[2]);
+      q[k][0] = bf2f((uint16_t)(w.lo & 0xffffu));
+      q[k][1] = bf2f((uint16_t)(w.lo >> 16));
+      q[k][2] = bf2f((uint16_t)(w.hi & 0xffffu));
     } else {
-      const uint32_t pr = *reinterpret_cast<const uint32_t *>(pp + 1);
-      q[k][0] = bf2f(pp[0]);
-      q[k][1] = bf2f((uint16_t)(pr & 0xffffu));
-      q[k][2] = bf2f((uint16_t)(pr >> 16));
+      q[k][0] = bf2f((uint16_t)(w.lo >> 16));
+      q[k][1] = bf2f((uint16_t)(w.hi & 0xffffu));
+      q[k][2] = bf2f((uint16_t)(w.hi >> 16));
     }
   }
 #pragma unroll
@@ -324,7 +332,7 @@ extern "C" int dcvc_flow_warp(dcvc_tensor x, dcvc_tensor flow, dcvc_tensor y, co
       y.cstride % 8 == 0 && y.coff % 8 == 0 && flow.cstride % 2 == 0 && flow.coff % 2 == 0 &&
       ((uintptr_t)x.ptr & 15) == 0 && ((uintptr_t)y.ptr & 15) == 0 && ((uintptr_t)flow.ptr & 7) == 0) {
     const int64_t total = (int64_t)y.H * y.W * (y.C / 8);
-    hipLaunchKernelGGL(warp8_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, mk(x), mk(flow),
+    hipLaunchKernelGGL(warp8_kernel, dim3((unsigned)((total + 255) / 256 + 7) & ~7u), dim3(256), 0, st, mk(x), mk(flow),
                        mk(y), gx, gy);
     DCVC_LAUNCH_CHECK();
     return DCVC_HIP_OK;
