@@ -224,10 +224,11 @@ def test_frame_to_nhwc_padding(zero_pad):
     assert torch.equal(back(y), ref)
 
 
-def test_offset_diversity_matches_oracle():
+@pytest.mark.parametrize("H,W", [(24, 32), (6, 2), (10, 18)])
+def test_offset_diversity_matches_oracle(H, W):
+    # (6, 2): a one-column offset map; pixel pairs {2q-1, 2q} share its corners
     from oracle import dc_oracle as O
     h = K()
-    H, W = 24, 32
     feat = torch.randn(1, 48, H, W)
     flow = torch.randn(1, 2, H, W) * 3
     offs = torch.randn(1, 96, H // 2, W // 2) * 0.05
