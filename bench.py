@@ -29,6 +29,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 PEAK_BF16_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 PEAK_F32_TFLOPS = 157.3
 PEAK_HBM_GBS = 8000.0
+BASELINE_METRIC = "encode+decode fps @1080p per GPU; bpp bit-exact + PSNR \u0394<1e-4 dB vs ref"
 
 
 def parse():
@@ -46,13 +47,17 @@ def parse():
                     help="config C4: DCVC-DC YUV420 source coded as YCbCr 4:4:4 (dist_in_yuv420), 3840x2160")
     ap.add_argument("--gop", type=int, default=32)
     ap.add_argument("--q_index", type=int, default=0)
-    ap.add_argument("--precision", choices=["fast", "parity"], default="fast")
+    ap.add_argument("--precision", choices=["fast", "parity", "fast-bf16-tail"], default="fast",
+                    help="fast = bf16 feature convs + fp32 entropy-parameter tail (BASELINE C2); parity = fp32 "
+                         "end to end; fast-bf16-tail = bf16 MFMA for the entropy-parameter tail too (labelled)")
     ap.add_argument("--stream_part", type=int, default=8,
                     help="rANS stream parts (the reference's --stream_part_i/p); parts code in parallel threads")
     ap.add_argument("--lanes", type=int, default=1, choices=[1],
                     help="GOP lanes per GPU.  Concurrent lanes (separate HIP streams / processes sharing the GPU) "
                          "are disabled: co-running codecs showed an encoder/decoder divergence (DESIGN.md §9)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=16,
+                    help="host threads for the cpu_baseline oracle run (capped at the cores this process may use)")
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--profile-out", default="", help="per-shape kernel timing JSON of one P-frame")
     a = ap.parse_args()
@@ -114,16 +119,38 @@ def shard_seed(rank):
     return 1 + rank
 
 
+def host_info():
+    """nproc, the cores this process may run on, and the CPU model."""
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except AttributeError:
+        usable = os.cpu_count() or 1
+    return {"nproc": os.cpu_count() or 1, "usable": usable, "cpu": model}
+
+
 def cpu_baseline(isd, psd, args):
-    """Oracle (PyTorch fp32 CPU restatement, pinned to the reference) on a
-    bounded sample: one I-frame (untimed) then one P-frame encode+decode in
-    write mode at a quarter of the 1088x1920 area; fps scaled by area."""
+    """Oracle (PyTorch fp32 CPU restatement, pinned to the reference) timed on
+    this host: one full-size I-frame and one full-size P-frame (1088x1920 for
+    C3), each compress + rANS encode + rANS decode + decompress in write mode,
+    in one process on `threads` cores; fps = the GOP average
+    gop / (t_I + (gop - 1) t_P).  No area scaling."""
     from oracle import dc_oracle as O
     from oracle import rans_oracle as R
-    from dcvc_amd.synth import moving_pattern, to_float
-    threads = min(16, os.cpu_count() or 1)
+    from dcvc_amd.synth import moving_pattern, moving_pattern_yuv420, to_float
+    info = host_info()
+    threads = max(1, min(args.cpu_threads, info["usable"]))
     torch.set_num_threads(threads)
-    h, w = 544, 960
+    h, w = args.height, args.width
+    Hp, Wp = (h + 15) // 16 * 16, (w + 15) // 16 * 16
     inet = O.IntraOracle(isd, R.pmf_to_quantized_cdf)
     pnet = O.DMCOracle(psd, R.pmf_to_quantized_cdf)
     tabs = {"i_y": (inet.y_cdf, inet.y_sizes, inet.y_offsets), "i_z": inet.z_tab,
@@ -144,7 +171,15 @@ def cpu_baseline(isd, psd, args):
             return v
         return decoder
 
-    frames = [torch.from_numpy(to_float(moving_pattern(h, w, t, seed=1))).unsqueeze(0) for t in range(2)]
+    def frame(t):
+        if args.yuv420:
+            from oracle.harness_oracle import yuv_u8_to_input
+            y, uv = moving_pattern_yuv420(h, w, t, seed=1)
+            return torch.from_numpy(yuv_u8_to_input(y, uv, Hp, Wp)).permute(2, 0, 1).unsqueeze(0).contiguous()
+        x = torch.from_numpy(to_float(moving_pattern(h, w, t, seed=1))).unsqueeze(0)
+        return torch.nn.functional.pad(x, (0, Wp - w, 0, Hp - h), mode="replicate")
+
+    frames = [frame(t) for t in range(2)]
     with torch.no_grad():
         t0 = time.time()
         dec = code(inet.compress(frames[0], False, args.q_index), "i_")
@@ -155,13 +190,13 @@ def cpu_baseline(isd, psd, args):
         dec = code(pnet.compress(frames[1], dpb, False, args.q_index, 1), "p_")
         pnet.decompress(dpb, dec, h, w, False, args.q_index, 1)
         t_p = time.time() - t0
-    Hp, Wp = (args.height + 15) // 16 * 16, (args.width + 15) // 16 * 16
-    area = (Hp * Wp) / (h * w)
     gop = args.gop
-    fps = gop / (area * (t_i + (gop - 1) * t_p))
+    fps = gop / (t_i + (gop - 1) * t_p)
     return {"value": fps, "unit": "frames/s", "cores": threads, "kind": "port",
-            "sample": f"oracle write-mode I+P encode+decode at {h}x{w} (I {t_i:.1f}s, P {t_p:.1f}s), "
-                      f"scaled x{area:.1f} by area to {Hp}x{Wp}, GOP {gop} average"}
+            "sample": f"oracle write-mode encode+decode of one full-size I-frame ({t_i:.1f} s) and one full-size "
+                      f"P-frame ({t_p:.1f} s) at {Hp}x{Wp}, {threads} torch threads in one process; fps = GOP "
+                      f"{gop} average; host nproc {info['nproc']}, usable {info['usable']}, CPU {info['cpu']}",
+            "ms_I": round(t_i * 1e3, 1), "ms_P": round(t_p * 1e3, 1)}
 
 
 def hem_q(sd_i, sd_p, rate):
@@ -172,14 +207,17 @@ def hem_q(sd_i, sd_p, rate):
 
 
 def cpu_baseline_hem(isd, psd, args):
-    """HEM oracle on the same bounded sample as cpu_baseline (one I-frame
-    untimed-ready, one P-frame, write mode, per-call rANS encode+decode)."""
+    """HEM oracle on the same sample as cpu_baseline: one full-size I-frame and
+    one full-size P-frame (zero-padded to a multiple of 64), write mode with
+    per-call rANS encode + decode, GOP average, no area scaling."""
     from oracle import hem_oracle as O
     from oracle import rans_oracle as R
     from dcvc_amd.synth import moving_pattern, to_float
-    threads = min(16, os.cpu_count() or 1)
+    info = host_info()
+    threads = max(1, min(args.cpu_threads, info["usable"]))
     torch.set_num_threads(threads)
-    h, w = 512, 960
+    h, w = args.height, args.width
+    Hp, Wp = (h + 63) // 64 * 64, (w + 63) // 64 * 64
     inet = O.IntraOracle(isd, R.pmf_to_quantized_cdf)
     pnet = O.DMCOracle(psd, R.pmf_to_quantized_cdf)
     tabs = {"i_y": inet.tab_y[:3], "i_z": inet.tab_z[:3], "p_y": pnet.tab_y[:3], "p_z": pnet.tab_z[:3],
@@ -196,22 +234,27 @@ def cpu_baseline_hem(isd, psd, args):
             return torch.from_numpy(R.hem_decode(st, idx.numpy(), *tabs[kind]).astype(np.int64))
         return decoder
 
-    frames = [torch.from_numpy(to_float(moving_pattern(h, w, t, seed=1))).unsqueeze(0) for t in range(2)]
+    def frame(t):
+        x = torch.from_numpy(to_float(moving_pattern(h, w, t, seed=1))).unsqueeze(0)
+        return torch.nn.functional.pad(x, (0, Wp - w, 0, Hp - h))
+
+    frames = [frame(t) for t in range(2)]
     with torch.no_grad():
         t0 = time.time()
-        xh = inet.decompress(coder(inet.compress(frames[0], qi)), h, w, qi)
+        xh = inet.decompress(coder(inet.compress(frames[0], qi)), Hp, Wp, qi)
         t_i = time.time() - t0
         dpb = {"ref_frame": xh, "ref_feature": None, "ref_y": None, "ref_mv_y": None}
         t0 = time.time()
-        pnet.decompress(dpb, coder(pnet.compress(frames[1], dpb, qmv, qy)), h, w, qmv, qy)
+        pnet.decompress(dpb, coder(pnet.compress(frames[1], dpb, qmv, qy)), Hp, Wp, qmv, qy)
         t_p = time.time() - t0
-    Hp, Wp = (args.height + 63) // 64 * 64, (args.width + 63) // 64 * 64
-    area = (Hp * Wp) / (h * w)
     gop = args.gop
-    fps = gop / (area * (t_i + (gop - 1) * t_p))
+    fps = gop / (t_i + (gop - 1) * t_p)
     return {"value": fps, "unit": "frames/s", "cores": threads, "kind": "port",
-            "sample": f"HEM oracle write-mode I+P encode+decode at {h}x{w} (I {t_i:.1f}s, P {t_p:.1f}s), "
-                      f"scaled x{area:.2f} by area to {Hp}x{Wp}, GOP {gop} average"}
+            "sample": f"HEM oracle write-mode encode+decode of one full-size I-frame ({t_i:.1f} s) and one "
+                      f"full-size P-frame ({t_p:.1f} s) at {Hp}x{Wp}, {threads} torch threads in one process; "
+                      f"fps = GOP {gop} average; host nproc {info['nproc']}, usable {info['usable']}, "
+                      f"CPU {info['cpu']}",
+            "ms_I": round(t_i * 1e3, 1), "ms_P": round(t_p * 1e3, 1)}
 
 
 def workload_key(argv):
@@ -272,7 +315,8 @@ def main():
         K.set_option(k, int(v))
     hem = args.model == "hem"
     isd, psd = make_weights(dist, rank, device, args.model)
-    prec = Precision.fast(latent_compute=K.BF16) if args.precision == "fast" else Precision.parity()
+    prec = {"fast": Precision.fast(), "parity": Precision.parity(),
+            "fast-bf16-tail": Precision.fast(latent_compute=K.BF16)}[args.precision]
     if hem:
         from dcvc_amd.hem import DMC, IntraNoAR
         qi, qmv, qy = hem_q(isd, psd, args.rate)
@@ -281,7 +325,15 @@ def main():
 
     h, w = args.height, args.width
     align = 64 if hem else 16     # HEM test_video.py:113-119 pads to 64, DC to 16
-    nframes = args.warmup + args.steps
+    # frame schedule: W warmup frames, then K timed frames starting at the next
+    # GOP boundary, so the timed window opens with an I-frame (an I-frame resets
+    # the DPB, test_video.py:140-150) and holds the IP=gop mix of the metric
+    start = -(-args.warmup // args.gop) * args.gop
+    warm_idx = list(range(args.warmup))
+    timed_idx = list(range(start, start + args.steps))
+    extra = start + args.steps if (start + args.steps) % args.gop else start + args.steps + 1
+    sched = warm_idx + timed_idx + [extra]
+    nframes = len(sched)
     out_root = f"/dev/shm/dcvc_bench_{os.getpid()}"
 
     class Lane:
@@ -309,17 +361,18 @@ def main():
             # sums) is part of the step
             self.stage = FrameStage(h, w, align, args.yuv420, zero_pad=hem, frame_num=nframes + 2, device=device)
             t0 = l * args.gop
+            self.slot = {t: n for n, t in enumerate(sched)}
             if args.yuv420:
-                self.frames = [tuple(torch.from_numpy(a).to(device)
-                                     for a in moving_pattern_yuv420(h, w, t0 + t, seed=shard_seed(rank)))
-                               for t in range(nframes)]
+                self.frames = {t: tuple(torch.from_numpy(a).to(device)
+                                        for a in moving_pattern_yuv420(h, w, t0 + t, seed=shard_seed(rank)))
+                               for t in sched}
             else:
-                self.frames = [torch.from_numpy(moving_pattern(h, w, t0 + t, seed=shard_seed(rank))).to(device)
-                               for t in range(nframes)]
+                self.frames = {t: torch.from_numpy(moving_pattern(h, w, t0 + t, seed=shard_seed(rank))).to(device)
+                               for t in sched}
             self.out_dir = os.path.join(out_root, str(l))
             os.makedirs(self.out_dir, exist_ok=True)
             self.dpb = None
-            self.bits, self.kinds, self.per = [], [], []
+            self.bits, self.kinds, self.per = {}, {}, []
 
         def step(self, i):
             # uint8 source -> padded NHWC: replicate (DC test_video.py:130) / zeros (HEM)
@@ -330,28 +383,28 @@ def main():
                 if i % args.gop == 0:
                     r = inet.encode_decode(x, qi, path, pic_width=w, pic_height=h)
                     self.dpb = {"ref_frame": r["x_hat"], "ref_feature": None, "ref_y": None, "ref_mv_y": None}
-                    self.kinds.append("I")
+                    self.kinds[i] = "I"
                 else:
                     r = pnet.encode_decode(x, self.dpb, path, pic_width=w, pic_height=h,
                                            mv_y_q_scale=qmv, y_q_scale=qy)
                     self.dpb = r["dpb"]
-                    self.kinds.append("P")
+                    self.kinds[i] = "P"
             elif i % args.gop == 0:
                 r = inet.encode_decode(x, False, args.q_index, path, pic_width=w, pic_height=h)
                 self.dpb = {"ref_frame": r["x_hat"], "ref_feature": None, "ref_mv_feature": None,
                             "ref_y": None, "ref_mv_y": None}
-                self.kinds.append("I")
+                self.kinds[i] = "I"
             else:
                 r = pnet.encode_decode(x, self.dpb, False, args.q_index, path, pic_width=w, pic_height=h,
                                        frame_idx=i % 4)
                 self.dpb = r["dpb"]
-                self.kinds.append("P")
-            self.bits.append(r["bit"])
-            self.stage.distortion(self.dpb["ref_frame"], self.frames[i], i)
+                self.kinds[i] = "P"
+            self.bits[i] = r["bit"]
+            self.stage.distortion(self.dpb["ref_frame"], self.frames[i], self.slot[i])
 
-        def run(self, lo, hi, timed):
+        def run(self, idx, timed):
             with torch.cuda.device(device), torch.cuda.stream(self.stream):
-                for i in range(lo, hi):
+                for i in idx:
                     ts = time.time()
                     self.step(i)
                     if timed:
@@ -362,23 +415,23 @@ def main():
     H, W = lanes[0].stage.H, lanes[0].stage.W
     torch.cuda.synchronize(device)   # setup work on the default stream is done before lanes start
 
-    def run_all(lo, hi, timed):
+    def run_all(idx, timed):
         for ln in lanes:
-            ln.run(lo, hi, timed)
+            ln.run(idx, timed)
 
-    run_all(0, args.warmup, False)
+    run_all(warm_idx, False)
     torch.cuda.synchronize(device)
     if dist is not None:
         dist.barrier()
     t0 = time.time()
-    run_all(args.warmup, nframes, True)
+    run_all(timed_idx, True)
     torch.cuda.synchronize(device)
     if dist is not None:
         dist.barrier()
     elapsed = max_over_ranks(dist, time.time() - t0, device)
 
     def step(i):   # one more frame on lane 0 (the roofline P-frame below)
-        lanes[0].run(i, i + 1, False)
+        lanes[0].run([i], False)
 
     # ---- roofline of the dominant kernel, from per-launch HIP events recorded
     # on the stream the kernels run on, over one extra P-frame.  "Dominant" =
@@ -387,7 +440,7 @@ def main():
     roof = None
     if not args.no_roofline and rank == 0:
         K.PROFILE = []
-        step(nframes - 1 if (nframes - 1) % args.gop else nframes - 2)
+        step(extra)
         torch.cuda.synchronize(device)
         fam, shapes = {}, {}
         for f, e0, e1, fl, nb, key in K.PROFILE:
@@ -406,7 +459,7 @@ def main():
                             "tflops": round(v[1] / max(v[0], 1e-12) / 1e12, 2),
                             "gbs": round(v[2] / max(v[0], 1e-12) / 1e9, 1)} for k, v in rows], f, indent=0)
         key, (tsec, fl, nb, n) = rows[0]
-        peak_f = PEAK_BF16_TFLOPS if args.precision == "fast" else PEAK_F32_TFLOPS
+        peak_f = PEAK_F32_TFLOPS if args.precision == "parity" else PEAK_BF16_TFLOPS
         t_mfma, t_hbm = fl / (peak_f * 1e12), nb / (PEAK_HBM_GBS * 1e9)
         if t_mfma >= t_hbm:
             ach = fl / tsec / 1e12
@@ -446,7 +499,7 @@ def main():
                                    "gbytes": round(sum(v[2] for v in shapes.values()) / 1e9, 2)}
 
     if rank == 0:
-        kinds = [k for ln in lanes for k in ln.kinds[args.warmup:nframes]]
+        kinds = [ln.kinds[i] for ln in lanes for i in timed_idx]
         per = [p for ln in lanes for p in ln.per]
         n_i = kinds.count("I")
         ti = [p for p, k in zip(per, kinds) if k == "I"]
@@ -454,8 +507,8 @@ def main():
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             cpu = cpu_baseline_hem(isd, psd, args) if hem else cpu_baseline(isd, psd, args)
-        timed_bits = [b for ln in lanes for b in ln.bits[args.warmup:nframes]]
-        sse = np.concatenate([ln.stage.sums()[args.warmup:nframes] for ln in lanes])
+        timed_bits = [ln.bits[i] for ln in lanes for i in timed_idx]
+        sse = np.concatenate([ln.stage.sums()[[ln.slot[i] for i in timed_idx]] for ln in lanes])
         if args.yuv420:
             per = [psnr_yuv(e, h, w) for e in sse]
             psnr = {"psnr": round(float(np.mean([p[3] for p in per])), 4),
@@ -463,8 +516,7 @@ def main():
         else:
             psnr = {"psnr": round(float(np.mean([psnr_rgb(e, h, w) for e in sse])), 4)}
         line = {
-            "metric": f"encode+decode fps @{h}p per GPU ({'DCVC-HEM' if hem else 'DCVC-DC'} write mode, "
-                      "real bitstreams)",
+            "metric": BASELINE_METRIC,
             "value": round(world * args.lanes * args.steps / elapsed, 4),
             "unit": "frames/s",
             "n_gpus": world,
@@ -474,7 +526,8 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "bf16" if args.precision == "fast" else "f32",
+            "dtype": {"fast": "bf16 features, fp32 entropy params", "parity": "f32",
+                      "fast-bf16-tail": "bf16 (entropy-parameter tail in bf16 too)"}[args.precision],
             "data": "synthetic (moving sinusoid + noise frames, seeded random weights)",
             "config": {"workload": (f"C2 DCVC-HEM RGB {w}x{h} (zero pad {W}x{H}) IP={args.gop} write mode"
                                     if hem else
@@ -487,8 +540,11 @@ def main():
                        "I_frames_timed": n_i,
                        "ms_I": round(1e3 * float(np.mean(ti)), 2) if ti else None,
                        "ms_P": round(1e3 * float(np.mean(tp)), 2) if tp else None,
+                       "timed_frames": [timed_idx[0], timed_idx[-1]],
+                       **({"fps_gop_avg": round(args.gop / (float(np.mean(ti)) + (args.gop - 1) * float(np.mean(tp))),
+                                                 3)} if ti and tp else {}),
                        "bpp": round(float(np.mean(timed_bits)) / (h * w), 5), **psnr,
-                       **({"bits_per_lane": [int(sum(ln.bits[args.warmup:nframes])) for ln in lanes]}
+                       **({"bits_per_lane": [int(sum(ln.bits[i] for i in timed_idx)) for ln in lanes]}
                           if args.lanes > 1 else {})},
             "roofline": roof,
             "cpu_baseline": cpu,

@@ -512,6 +512,9 @@ extern "C" int64_t dcvc_conv_pack_weights(const float *w, int cout, int cin, int
 }
 
 extern "C" int dcvc_internal_gemm1x1(const dcvc_conv_args *a, void *stream);
+extern "C" int dcvc_internal_gemm1x1_f32(const dcvc_conv_args *a, void *stream);
+extern "C" void dcvc_internal_gemm1x1_f32_enable(int v);
+extern "C" void dcvc_internal_gemm1x1_f32_cfg(int v);
 extern "C" int dcvc_internal_conv3x3(const dcvc_conv_args *a, void *stream);
 extern "C" void dcvc_internal_conv3x3_resident(int v);
 extern "C" void dcvc_internal_conv3p_enable(int v);
@@ -578,6 +581,10 @@ extern "C" int dcvc_conv2d(const dcvc_conv_args *a, void *stream) {
     const int r = dcvc_internal_gemm1x1(a, stream);
     if (r != DCVC_HIP_EUNSUPPORTED) return r;
   }
+  if (a->kh == 1 && a->kw == 1 && a->stride == 1 && a->compute == DCVC_F32) {
+    const int r = dcvc_internal_gemm1x1_f32(a, stream);
+    if (r != DCVC_HIP_EUNSUPPORTED) return r;
+  }
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const bool xin32 = a->x.dtype == DCVC_F32, yout32 = a->y.dtype == DCVC_F32;
   {
@@ -604,6 +611,14 @@ extern "C" int dcvc_set_option(const char *name, int value) {
   if (!name) return DCVC_HIP_EINVAL;
   if (std::strcmp(name, "gemm1x1") == 0) {
     g_use_gemm = value;
+    return DCVC_HIP_OK;
+  }
+  if (std::strcmp(name, "gemm1x1_f32") == 0) {
+    dcvc_internal_gemm1x1_f32_enable(value);
+    return DCVC_HIP_OK;
+  }
+  if (std::strcmp(name, "gemm1x1_f32_cfg") == 0) {
+    dcvc_internal_gemm1x1_f32_cfg(value);
     return DCVC_HIP_OK;
   }
   if (std::strcmp(name, "conv3x3") == 0) {

@@ -1,0 +1,289 @@
+// Pointwise (1x1, stride 1) convolution in fp32 (f32 in, f32 MFMA, f32 out):
+// the entropy-parameter tail of the codecs (hyperprior decoders, prior
+// fusion, the quadtree / dual spatial priors: DepthConvBlocks on the
+// 68x120 latent grid at 1080p) that the reference computes in fp32.
+//
+// D[n][p] = sum_k W[n][k] * X[p][k] on v_mfma_f32_16x16x4_f32 (exact f32,
+// the same accumulation order as conv.hip's f32 path: k ascending, 4 per
+// MFMA, so the two kernels are bit-identical).  Workgroup = 4 waves = BM
+// pixels x BN channels; K advances 32 channels per step.  Each step's global
+// loads (32 B per lane) are issued into registers before the MFMAs of the
+// previous step and written to the other LDS buffer after them (one barrier
+// per step), so the load latency hides behind the matrix work; conv.hip's
+// generic path waited on it twice per 32 channels (47 TF/s at 384->384,
+// 68x120).  LDS rows are 36 floats: the 16 lanes x 4 k of an operand read
+// (rows r..r+15, k..k+3) fall on 64 distinct banks.  Epilogue: epilogue.h.
+#include "common.h"
+#include "epilogue.h"
+
+namespace {
+
+constexpr int kK = 32;   // weight rows are padded to 32 channels (conv.hip's chunk)
+
+struct GF {
+  const float *x;
+  int M, W;
+  int xcs, xco;
+  const float *w;  // [cout][wstride] f32 (dcvc_conv_pack_weights, compute f32)
+  const float *bias;
+  void *y;
+  int ycs, yco;
+  int cin, cout, wstride;
+  int in_op;
+  float in_slope;
+  int act;
+  float slope;
+  int shuffle;
+  const float *scale;
+  const void *res;
+  int rcs, rco;
+  const void *res2;
+  int r2cs, r2co;
+  int Wout;
+  int vec_out;
+  int tiles_m;
+};
+
+// LDS row stride: KK + 4 floats, so the 16 lanes x 4 k of an operand read hit
+// 64 distinct banks
+template <int KK> __host__ __device__ constexpr int ldk() { return KK + 4; }
+
+template <int BM, int BN, int KK>
+__host__ __device__ constexpr size_t lds_main() {
+  return (size_t)2 * (BM + BN) * ldk<KK>() * 4 > (size_t)BM * (BN + 4) * 4 ? (size_t)2 * (BM + BN) * ldk<KK>() * 4
+                                                                            : (size_t)BM * (BN + 4) * 4;
+}
+
+template <int BM, int BN, int WMW, int KK>
+__global__ void __launch_bounds__(256) gemm1x1f_kernel(GF p) {
+  constexpr int kLD = ldk<KK>();
+  constexpr int Q = KK / 8;                 // 8-float pieces per row per step
+  constexpr int WNW = 4 / WMW;
+  constexpr int TM = BM / WMW / 16;
+  constexpr int TN = BN / WNW / 16;
+  constexpr int PX = (BM * Q + 255) / 256;  // 8-float pieces per thread per step
+  constexpr int PW = (BN * Q + 255) / 256;
+  static_assert(TM >= 1 && TN >= 1, "tile");
+  extern __shared__ __align__(16) unsigned char smem[];
+  float *Xs = reinterpret_cast<float *>(smem);  // [2][BM][kLD]
+  float *Ws = Xs + 2 * BM * kLD;                 // [2][BN][kLD]
+  float *Lc = reinterpret_cast<float *>(smem + lds_main<BM, BN, KK>());
+
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int wm = wave % WMW, wn = wave / WMW;
+  const int tm = blockIdx.x % p.tiles_m, tn = blockIdx.x / p.tiles_m;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int nsteps = (p.wstride + KK - 1) / KK;
+  epi::stage_consts(p, Lc, n0, BN);
+
+  float4 pxa[PX], pxb[PX], pwa[PW], pwb[PW];
+  auto load_step = [&](int s) {
+    const int k0 = s * KK;
+#pragma unroll
+    for (int i = 0; i < PX; ++i) {
+      const int it = threadIdx.x + i * 256;
+      const int r = it / Q, q = it % Q;
+      const int m = m0 + r, c = k0 + q * 8;
+      if (it < BM * Q && m < p.M && c < p.cin) {
+        const float *src = p.x + (int64_t)m * p.xcs + p.xco + c;
+        pxa[i] = *reinterpret_cast<const float4 *>(src);
+        pxb[i] = *reinterpret_cast<const float4 *>(src + 4);
+      } else {
+        pxa[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+        pxb[i] = pxa[i];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < PW; ++i) {
+      const int it = threadIdx.x + i * 256;
+      const int r = it / Q, q = it % Q;
+      const int n = n0 + r, c = k0 + q * 8;
+      if (it < BN * Q && n < p.cout && c < p.wstride) {
+        const float *src = p.w + (int64_t)n * p.wstride + c;
+        pwa[i] = *reinterpret_cast<const float4 *>(src);
+        pwb[i] = *reinterpret_cast<const float4 *>(src + 4);
+      } else {
+        pwa[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+        pwb[i] = pwa[i];
+      }
+    }
+  };
+  auto lrelu4 = [&](float4 v) {
+    const float s = p.in_slope;
+    v.x = v.x >= 0.f ? v.x : v.x * s;
+    v.y = v.y >= 0.f ? v.y : v.y * s;
+    v.z = v.z >= 0.f ? v.z : v.z * s;
+    v.w = v.w >= 0.f ? v.w : v.w * s;
+    return v;
+  };
+  auto store_step = [&](int buf) {
+    float *xs = Xs + buf * BM * kLD;
+    float *ws = Ws + buf * BN * kLD;
+#pragma unroll
+    for (int i = 0; i < PX; ++i) {
+      const int it = threadIdx.x + i * 256;
+      if (BM * Q % 256 == 0 || it < BM * Q) {
+        const int r = it / Q, q = it % Q;
+        float4 a = pxa[i], b = pxb[i];
+        if (p.in_op == DCVC_IN_LRELU) {
+          a = lrelu4(a);
+          b = lrelu4(b);
+        }
+        *reinterpret_cast<float4 *>(xs + r * kLD + q * 8) = a;
+        *reinterpret_cast<float4 *>(xs + r * kLD + q * 8 + 4) = b;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < PW; ++i) {
+      const int it = threadIdx.x + i * 256;
+      if (BN * Q % 256 == 0 || it < BN * Q) {
+        const int r = it / Q, q = it % Q;
+        *reinterpret_cast<float4 *>(ws + r * kLD + q * 8) = pwa[i];
+        *reinterpret_cast<float4 *>(ws + r * kLD + q * 8 + 4) = pwb[i];
+      }
+    }
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int col = lane & 15, hi = lane >> 4;
+  load_step(0);
+  store_step(0);
+  __syncthreads();
+  for (int s = 0; s < nsteps; ++s) {
+    const int buf = s & 1;
+    if (s + 1 < nsteps) load_step(s + 1);
+    const float *xs = Xs + buf * BM * kLD;
+    const float *ws = Ws + buf * BN * kLD;
+#pragma unroll
+    for (int g = 0; g < KK / 4; ++g) {
+      float a[TN], b[TM];
+#pragma unroll
+      for (int j = 0; j < TN; ++j) a[j] = ws[((wn * TN + j) * 16 + col) * kLD + g * 4 + hi];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) b[i] = xs[((wm * TM + i) * 16 + col) * kLD + g * 4 + hi];
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[j], b[i], acc[i][j], 0, 0, 0);
+    }
+    if (s + 1 < nsteps) store_step(buf ^ 1);
+    __syncthreads();
+  }
+
+  float *T = reinterpret_cast<float *>(smem);
+  constexpr int LD = BN + 4;
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+      epi::put4(p, T, LD, (wm * TM + i) * 16 + col, (wn * TN + j) * 16 + hi * 4, Lc, acc[i][j]);
+  __syncthreads();
+  epi::store_tile<float, epi::ipt(BM, BN, 256)>(p, T, LD, BM, n0, min(BN, p.cout - n0), Lc, BN,
+                                                [&](int l, int &oy, int &ox) {
+    const int m = m0 + l;
+    oy = m / p.W;
+    ox = m - oy * p.W;
+    return m < p.M;
+  });
+}
+
+template <int BM, int BN, int WMW, int KK>
+int launch(GF p, hipStream_t st) {
+  p.tiles_m = (p.M + BM - 1) / BM;
+  const int tiles_n = (p.cout + BN - 1) / BN;
+  const size_t lds = lds_main<BM, BN, KK>() + epi::consts_floats(BN) * 4;
+  auto kern = gemm1x1f_kernel<BM, BN, WMW, KK>;
+  dcvc_note_kernel("gemm1x1f_kernel<%d, %d, %d, %d>@%lld", BM, BN, WMW, KK, (long long)p.tiles_m * tiles_n * 256);
+  if (lds > 64 * 1024) dcvc_ensure_lds(reinterpret_cast<const void *>(kern), (int)lds);
+  hipLaunchKernelGGL(kern, dim3((unsigned)(p.tiles_m * tiles_n)), dim3(256), lds, st, p);
+  DCVC_LAUNCH_CHECK();
+  return DCVC_HIP_OK;
+}
+
+int g_use_gemm_f32 = 1;
+int g_cfg = 0;  // dcvc_set_option("gemm1x1_f32_cfg", i): force tile config i (A/B), 0 = automatic
+
+// Tile choice: the widest BN in {128, 64, 32} whose grid still has >= 512
+// workgroups at BM = 64 (two per CU or more: the f32 MFMA loop is long, so
+// fewer, fuller tiles win while every CU has work); narrower maps fall back
+// to 32-pixel tiles.
+int dispatch(const GF &p, hipStream_t st) {
+  switch (g_cfg) {
+    case 1: return launch<64, 64, 2, 32>(p, st);
+    case 2: return launch<64, 64, 2, 64>(p, st);
+    case 3: return launch<64, 128, 2, 32>(p, st);
+    case 4: return launch<128, 64, 2, 32>(p, st);
+    case 5: return launch<128, 128, 2, 32>(p, st);
+    case 6: return launch<64, 128, 2, 64>(p, st);
+    case 7: return launch<32, 64, 2, 32>(p, st);
+    case 8: return launch<64, 32, 4, 32>(p, st);
+    case 9: return launch<32, 128, 1, 32>(p, st);
+    case 10: return launch<128, 32, 4, 32>(p, st);
+    case 11: return launch<64, 32, 4, 64>(p, st);
+    default: break;
+  }
+  auto blocks = [&](int bm, int bn) { return (long)((p.M + bm - 1) / bm) * ((p.cout + bn - 1) / bn); };
+  if (p.cout > 64 && blocks(64, 128) >= 512) return launch<64, 128, 2, 32>(p, st);
+  if (p.cout > 32 && blocks(64, 64) >= 512) return launch<64, 64, 2, 32>(p, st);
+  if (blocks(64, 32) >= 512) return launch<64, 32, 4, 32>(p, st);
+  if (p.cout > 32) return launch<32, 64, 2, 32>(p, st);
+  return launch<32, 32, 2, 32>(p, st);
+}
+
+}  // namespace
+
+// Called by dcvc_conv2d for 1x1 stride-1 convs with f32 compute, f32 in/out
+// and 32-byte-aligned channel views; returns DCVC_HIP_EUNSUPPORTED otherwise.
+extern "C" int dcvc_internal_gemm1x1_f32(const dcvc_conv_args *a, void *stream) {
+  if (!g_use_gemm_f32) return DCVC_HIP_EUNSUPPORTED;
+  if (a->kh != 1 || a->kw != 1 || a->stride != 1 || a->compute != DCVC_F32) return DCVC_HIP_EUNSUPPORTED;
+  if (a->in_op != DCVC_IN_NONE && a->in_op != DCVC_IN_LRELU) return DCVC_HIP_EUNSUPPORTED;
+  if (a->x.dtype != DCVC_F32 || a->y.dtype != DCVC_F32) return DCVC_HIP_EUNSUPPORTED;
+  if (a->cin % 8 || a->x.cstride % 4 || a->x.coff % 4 || ((uintptr_t)a->x.ptr & 15) || ((uintptr_t)a->w & 15))
+    return DCVC_HIP_EUNSUPPORTED;
+  GF p{};
+  p.x = reinterpret_cast<const float *>(a->x.ptr);
+  p.M = a->x.H * a->x.W;
+  p.W = a->x.W;
+  p.xcs = a->x.cstride;
+  p.xco = a->x.coff;
+  p.w = reinterpret_cast<const float *>(a->w);
+  p.bias = a->bias;
+  p.y = a->y.ptr;
+  p.ycs = a->y.cstride;
+  p.yco = a->y.coff;
+  p.cin = a->cin;
+  p.cout = a->cout;
+  p.wstride = (a->cin + kK - 1) / kK * kK;  // packed row length; steps of KK = 64 read zeros past it
+  p.in_op = a->in_op;
+  p.in_slope = a->in_slope;
+  p.act = a->act;
+  p.slope = a->slope;
+  p.shuffle = a->shuffle;
+  p.scale = a->scale;
+  p.Wout = a->y.W;
+  if (a->res.ptr) {
+    p.res = a->res.ptr;
+    p.rcs = a->res.cstride;
+    p.rco = a->res.coff;
+  }
+  if (a->res2.ptr) {
+    p.res2 = a->res2.ptr;
+    p.r2cs = a->res2.cstride;
+    p.r2co = a->res2.coff;
+  }
+  bool vo = (p.ycs % 8 == 0) && (p.yco % 8 == 0) && (((uintptr_t)p.y & 15) == 0);
+  if (a->res.ptr) vo = vo && (p.rcs % 8 == 0) && (p.rco % 8 == 0) && (((uintptr_t)p.res & 15) == 0);
+  if (a->res2.ptr) vo = vo && (p.r2cs % 8 == 0) && (p.r2co % 8 == 0) && (((uintptr_t)p.res2 & 15) == 0);
+  p.vec_out = vo ? 1 : 0;
+  return dispatch(p, reinterpret_cast<hipStream_t>(stream));
+}
+
+extern "C" void dcvc_internal_gemm1x1_f32_enable(int v) { g_use_gemm_f32 = v; }
+extern "C" void dcvc_internal_gemm1x1_f32_cfg(int v) { g_cfg = v; }

@@ -303,9 +303,14 @@ def bit_estimator_cdf(P, p, x):
 
 def build_indexes(scales, log_min, step):
     """GaussianEncoder.build_indexes (models/entropy_models.py:269-273)."""
+    return index_float(scales, log_min, step).clamp_(0, 255).int()
+
+
+def index_float(scales, log_min, step):
+    """build_indexes before the clamp and the int() truncation (the value whose
+    distance to an integer says how close an index is to flipping)."""
     scales = torch.maximum(scales, torch.zeros_like(scales) + 1e-5)
-    idx = (torch.log(scales) - log_min) / step
-    return idx.clamp_(0, 255).int()
+    return (torch.log(scales) - log_min) / step
 
 
 def probs_to_bits(probs):
@@ -362,9 +367,11 @@ def _masked(y, scales, means, mask):
 STEP_MASK = ((0, 1, 2, 3), (3, 2, 1, 0), (2, 3, 0, 1), (1, 0, 3, 2))
 
 
-def four_part_prior(P, y, common_params, adaptors, spatial):
+def four_part_prior(P, y, common_params, adaptors, spatial, yres_out=None):
     """forward_four_part_prior with write=True (common_model.py:142-252).
-    Returns (per-step symbols y_q_w_k, per-step scales_w_k, y_q, y_hat, scales_hat)."""
+    Returns (per-step symbols y_q_w_k, per-step scales_w_k, y_q, y_hat, scales_hat).
+    ``yres_out`` (a list) receives each step's pre-rounding y - means in the
+    layout of y_q_w_k (test instrumentation: distance to a rounding tie)."""
     quant_step, scales, means = common_params.chunk(3, 1)
     _, _, H, W = y.size()
     masks = four_part_masks(H, W)
@@ -398,6 +405,8 @@ def four_part_prior(P, y, common_params, adaptors, spatial):
         mks = STEP_MASK[step]
         sym_w.append(res[0][mks[0]][1] + res[1][mks[1]][1] + res[2][mks[2]][1] + res[3][mks[3]][1])
         sc_w.append(res[0][mks[0]][3] + res[1][mks[1]][3] + res[2][mks[2]][3] + res[3][mks[3]][3])
+        if yres_out is not None:
+            yres_out.append(res[0][mks[0]][0] + res[1][mks[1]][0] + res[2][mks[2]][0] + res[3][mks[3]][0])
     return sym_w, sc_w, y_q, y_hat, scales_hat
 
 
@@ -619,31 +628,49 @@ class DMCOracle:
     _MV_AD = ["mv_y_spatial_prior_adaptor_1", "mv_y_spatial_prior_adaptor_2", "mv_y_spatial_prior_adaptor_3"]
     _Y_AD = ["y_spatial_prior_adaptor_1", "y_spatial_prior_adaptor_2", "y_spatial_prior_adaptor_3"]
 
-    def compress(self, x, dpb, q_in_ckpt, q_index, frame_idx):
+    def compress(self, x, dpb, q_in_ckpt, q_index, frame_idx, tap=None, recon=False):
         """compress (video_model.py:425-481) minus the encoder-side
         reconstruction, whose output is unused in write mode.  Returns the
-        ordered list of coder calls [(kind, symbols, indexes)] and the dpb."""
+        ordered list of coder calls [(kind, symbols, indexes)] and the dpb.
+
+        Test instrumentation: ``tap`` (a dict) receives, per coder call, the
+        pre-rounding values ("pre": z or y - means) and the pre-truncation
+        scale indexes ("idx_f", y calls), plus the calls in dependency order
+        ("order": mv_z, mv_y steps, z, y steps).  ``recon=True`` also returns
+        the decoder-side dpb, built from the encoder's y_hat (the same values
+        decompress() reconstructs from the stream)."""
         P = self.P
         mv_q_enc, mv_q_dec, y_q_enc, y_q_dec = self.get_q(q_in_ckpt, q_index)
         est_mv = spynet(P, "optic_flow", x, dpb["ref_frame"])
         mv_y = mv_enc(P, "mv_encoder", est_mv, dpb["ref_mv_feature"], mv_q_enc)
         mv_y_pad, ss = pad_for_y(mv_y)
-        mv_z_hat = torch.round(hyper_enc(P, "mv_hyper_prior_encoder", mv_y_pad, False))
+        mv_z = hyper_enc(P, "mv_hyper_prior_encoder", mv_y_pad, False)
+        mv_z_hat = torch.round(mv_z)
         mv_params = self.mv_prior(mv_z_hat, dpb, ss)
+        mv_res, y_res = [], []
         mv_sym, mv_sc, _, mv_y_hat, _ = four_part_prior(P, mv_y, mv_params, self._MV_AD,
-                                                        self.spatial("mv_y_spatial_prior"))
+                                                        self.spatial("mv_y_spatial_prior"), mv_res)
         mv_hat, mv_feature = mv_dec(P, "mv_decoder", mv_y_hat, mv_q_dec)
         c1, c2, c3 = self.motion_compensation(dpb, mv_hat, frame_idx)
         y = contextual_encoder(P, "contextual_encoder", x, c1, c2, c3, y_q_enc)
         y_pad, ss = pad_for_y(y)
-        z_hat = torch.round(hyper_enc(P, "contextual_hyper_prior_encoder", y_pad, True))
+        z = hyper_enc(P, "contextual_hyper_prior_encoder", y_pad, True)
+        z_hat = torch.round(z)
         params = self.res_prior(z_hat, dpb, c3, ss)
-        y_sym, y_sc, _, y_hat, _ = four_part_prior(P, y, params, self._Y_AD, self.spatial("y_spatial_prior"))
+        y_sym, y_sc, _, y_hat, _ = four_part_prior(P, y, params, self._Y_AD, self.spatial("y_spatial_prior"), y_res)
         calls = [("mvz", mv_z_hat, channel_indexes(mv_z_hat)), ("z", z_hat, channel_indexes(z_hat))]
         for s, sc in zip(mv_sym, mv_sc):
             calls.append(("y", s, build_indexes(sc, self.log_min, self.log_step)))
         for s, sc in zip(y_sym, y_sc):
             calls.append(("y", s, build_indexes(sc, self.log_min, self.log_step)))
+        if tap is not None:
+            tap["pre"] = [mv_z, z] + mv_res + y_res
+            tap["idx_f"] = [None, None] + [index_float(sc, self.log_min, self.log_step) for sc in mv_sc + y_sc]
+            tap["order"] = [0, 2, 3, 4, 5, 1, 6, 7, 8, 9]
+        if recon:
+            x_hat, feature = self.recon(y_hat, c1, c2, c3, y_q_dec)
+            return calls, {"ref_frame": x_hat, "ref_feature": feature, "ref_mv_feature": mv_feature,
+                           "ref_y": y_hat, "ref_mv_y": mv_y_hat}
         return calls
 
     def decompress(self, dpb, decoder, height, width, q_in_ckpt, q_index, frame_idx):
@@ -784,16 +811,29 @@ class IntraOracle:
 
     _AD = ["y_spatial_prior_adaptor_1", "y_spatial_prior_adaptor_2", "y_spatial_prior_adaptor_3"]
 
-    def compress(self, x, q_in_ckpt, q_index):
-        """compress (image_model.py:198-229) without the unused encoder recon."""
-        q_enc, _ = self.get_q(q_in_ckpt, q_index)
+    def compress(self, x, q_in_ckpt, q_index, tap=None, recon=False):
+        """compress (image_model.py:198-229) without the unused encoder recon;
+        ``tap`` / ``recon`` as in DMCOracle.compress."""
+        q_enc, q_dec = self.get_q(q_in_ckpt, q_index)
         y = self.enc(x, q_enc)
-        z_hat, ss = self.hyper(y)
+        y_pad, ss = pad_for_y(y)
+        P = self.P
+        z = depth_conv_block2(P, "hyper_enc.0", y_pad)
+        z = lrelu(conv(P, "hyper_enc.1", z, stride=2))
+        z = conv(P, "hyper_enc.3", z, stride=2)
+        z_hat = torch.round(z)
         params = self.prior(z_hat, ss)
-        sym, sc, _, _, _ = four_part_prior(self.P, y, params, self._AD, self.spatial)
+        y_res = []
+        sym, sc, _, y_hat, _ = four_part_prior(self.P, y, params, self._AD, self.spatial, y_res)
         calls = [("z", z_hat, channel_indexes(z_hat))]
         for s, c in zip(sym, sc):
             calls.append(("y", s, build_indexes(c, self.log_min, self.log_step)))
+        if tap is not None:
+            tap["pre"] = [z] + y_res
+            tap["idx_f"] = [None] + [index_float(c, self.log_min, self.log_step) for c in sc]
+            tap["order"] = [0, 1, 2, 3, 4]
+        if recon:
+            return calls, self.refine(self.dec(y_hat, q_dec)).clamp_(0, 1)
         return calls
 
     def decompress(self, decoder, height, width, q_in_ckpt, q_index):

@@ -17,7 +17,7 @@ import torch
 import torch.nn.functional as F
 
 from .dc_oracle import (Params, conv, lrelu, subpel, flow_warp, down2, spynet, EntropyTables, bit_estimator_cdf,
-                        build_indexes, laplace_bits, z_bits, probs_to_bits, get_downsampled_shape)
+                        build_indexes, index_float, laplace_bits, z_bits, probs_to_bits, get_downsampled_shape)
 
 CH_MV, CH_N, CH_M = 64, 64, 96  # models/video_model.py:140-142
 
@@ -149,8 +149,10 @@ def _masked(y, scales, means, mask):
     return y_res, y_q, y_q + means_hat, scales_hat
 
 
-def dual_prior(P, y, means, scales, quant_step, spatial, write=False):
-    """forward_dual_prior (models/common_model.py:102-156)."""
+def dual_prior(P, y, means, scales, quant_step, spatial, write=False, res_out=None):
+    """forward_dual_prior (models/common_model.py:102-156).  ``res_out`` (a
+    list) receives the two coder calls' pre-rounding y - means (test
+    instrumentation, tests/parity.py)."""
     _, _, H, W = y.size()
     m0, m1 = dual_masks(H, W)
     quant_step = torch.max(quant_step, torch.ones_like(quant_step) * 0.5)
@@ -168,6 +170,8 @@ def dual_prior(P, y, means, scales, quant_step, spatial, write=False):
     y_hat = torch.cat((h00 + h01, h11 + h10), dim=1)
     scales_hat = torch.cat((sh00 + sh01, sh11 + sh10), dim=1)
     y_hat = y_hat * quant_step
+    if res_out is not None:
+        res_out += [r00 + r11, r01 + r10]
     if write:
         return q00 + q11, q01 + q10, sh00 + sh11, sh01 + sh10, y_hat
     return y_q, y_hat, scales_hat
@@ -283,28 +287,46 @@ class DMCOracle:
     def spatial(self, prefix):
         return lambda t: seq3(self.P, prefix, t)
 
-    def compress(self, x, dpb, mv_y_q_scale, y_q_scale):
-        """compress (:263-330): the coder calls [(table, symbols, scales)]
-        and the (unused in write mode) encoder-side dpb."""
+    def compress(self, x, dpb, mv_y_q_scale, y_q_scale, tap=None, recon=False):
+        """compress (:263-330): the coder calls [(table, symbols, scales)].
+        Test instrumentation: ``tap`` (a dict) receives per call the
+        pre-rounding values ("pre"), the pre-truncation scale indexes
+        ("idx_f") and the dependency order; ``recon=True`` also returns the
+        decoder-side dpb built from the encoder's y_hat (what decompress()
+        reconstructs from the stream)."""
         P = self.P
         mvq = lower_bound_q(P, "mv_y_q_basic", mv_y_q_scale)
         yq = lower_bound_q(P, "y_q_basic", y_q_scale)
         est_mv = spynet(P, "optic_flow", x, dpb["ref_frame"])
         mv_y = enc_model(P, "mv_encoder", est_mv) / mvq
-        mv_z_hat = torch.round(hyper_enc(P, "mv_hyper_prior_encoder", mv_y))
+        mv_z = hyper_enc(P, "mv_hyper_prior_encoder", mv_y)
+        mv_z_hat = torch.round(mv_z)
         mv_q_step, mv_scales, mv_means = self.mv_params(mv_z_hat, dpb["ref_mv_y"], mv_y)
+        res = []
         mq0, mq1, ms0, ms1, mv_y_hat = dual_prior(P, mv_y, mv_means, mv_scales, mv_q_step,
-                                                  self.spatial("mv_y_spatial_prior"), write=True)
+                                                  self.spatial("mv_y_spatial_prior"), write=True, res_out=res)
         mv_y_hat = mv_y_hat * mvq
         mv_hat = dec_model(P, "mv_decoder", mv_y_hat)
         c1, c2, c3 = self.motion_compensation(dpb, mv_hat)
         y = self.contextual_encoder(x, c1, c2, c3) / yq
-        z_hat = torch.round(ctx_hyper_enc(P, y))
+        z = ctx_hyper_enc(P, y)
+        z_hat = torch.round(z)
         q_step, scales, means = self.y_params(z_hat, c3, dpb["ref_y"], y)
         q0, q1, s0, s1, y_hat = dual_prior(P, y, means, scales, q_step, self.spatial("y_spatial_prior"),
-                                           write=True)
-        return [("p_mvz", mv_z_hat, None), ("p_y", mq0, ms0), ("p_y", mq1, ms1), ("p_z", z_hat, None),
-                ("p_y", q0, s0), ("p_y", q1, s1)]
+                                           write=True, res_out=res)
+        calls = [("p_mvz", mv_z_hat, None), ("p_y", mq0, ms0), ("p_y", mq1, ms1), ("p_z", z_hat, None),
+                 ("p_y", q0, s0), ("p_y", q1, s1)]
+        if tap is not None:
+            lm, st = self.tab_y[3], self.tab_y[4]
+            tap["pre"] = [mv_z, res[0], res[1], z, res[2], res[3]]
+            tap["idx_f"] = [None if sc is None else index_float(sc, lm, st) for _, _, sc in calls]
+            tap["order"] = [0, 1, 2, 3, 4, 5]
+        if recon:
+            y_hat = y_hat * yq
+            feature, rec = self.recon(y_hat, c1, c2, c3)
+            return calls, {"ref_frame": rec.clamp(0, 1), "ref_feature": feature, "ref_y": y_hat,
+                           "ref_mv_y": mv_y_hat}
+        return calls
 
     def decompress(self, dpb, decoder, height, width, mv_y_q_scale, y_q_scale):
         """decompress (:332-375); decoder(kind, indexes) -> int symbols."""
@@ -388,15 +410,26 @@ class IntraOracle:
         P = self.P
         return conv(P, "refine.1", unet(P, "refine.0", dec_model(P, "dec", y_hat)))
 
-    def compress(self, x, q_scale):
+    def compress(self, x, q_scale, tap=None, recon=False):
+        """compress (:150-154); ``tap`` / ``recon`` as in DMCOracle.compress."""
         P = self.P
         q = lower_bound_q(P, "q_basic", q_scale)
         y = enc_model(P, "enc", x) / q
-        z_hat = torch.round(hyper_enc(P, "hyper_enc", y))
+        z = hyper_enc(P, "hyper_enc", y)
+        z_hat = torch.round(z)
         q_step, scales, means = self._prior(z_hat)
-        q0, q1, s0, s1, _ = dual_prior(P, y, means, scales, q_step, lambda t: seq3(P, "y_spatial_prior", t),
-                                       write=True)
-        return [("i_z", z_hat, None), ("i_y", q0, s0), ("i_y", q1, s1)]
+        res = []
+        q0, q1, s0, s1, y_hat = dual_prior(P, y, means, scales, q_step, lambda t: seq3(P, "y_spatial_prior", t),
+                                           write=True, res_out=res)
+        calls = [("i_z", z_hat, None), ("i_y", q0, s0), ("i_y", q1, s1)]
+        if tap is not None:
+            lm, st = self.tab_y[3], self.tab_y[4]
+            tap["pre"] = [z, res[0], res[1]]
+            tap["idx_f"] = [None, index_float(s0, lm, st), index_float(s1, lm, st)]
+            tap["order"] = [0, 1, 2]
+        if recon:
+            return calls, self._refine(y_hat * q).clamp_(0, 1)
+        return calls
 
     def decompress(self, decoder, height, width, q_scale):
         P = self.P

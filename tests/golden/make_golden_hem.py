@@ -126,9 +126,11 @@ def pad64(x):
     return torch.nn.functional.pad(x, (0, (64 - w % 64) % 64, 0, (64 - h % 64) % 64), mode="constant", value=0)
 
 
-def run_sequence(DMC, IntraNoAR, i_sd, p_sd, h, w, nframes, q, seed, out, tag):
+def run_sequence(DMC, IntraNoAR, i_sd, p_sd, h, w, nframes, q, seed, out, tag, frames=None, write_frames=None):
     """q = (i_frame_q_scale, p_frame_mv_y_q_scale, p_frame_y_q_scale), the
-    harness's args (test_video.py:126-141)."""
+    harness's args (test_video.py:126-141).  frames: optional list of float
+    (1, 3, h, w) frames (else the moving pattern of `seed`); write_frames:
+    how many frames write mode codes (default all)."""
     inet = IntraNoAR()
     inet.load_state_dict(i_sd)
     inet.eval()
@@ -154,12 +156,18 @@ def run_sequence(DMC, IntraNoAR, i_sd, p_sd, h, w, nframes, q, seed, out, tag):
         out[f"table_{name}_off"] = o
     qi, qmv, qy = q
     meta = {"h": h, "w": w, "frames": nframes, "q": list(q), "seed": seed, "write": [], "est": []}
-    with torch.no_grad():
-        dpb = None
+    if frames is None:
+        frames = []
         for t in range(nframes):
             u8 = moving_pattern(h, w, t, seed=seed)
             out[f"{tag}_frame{t}"] = u8
-            x = torch.from_numpy(to_float(u8)).unsqueeze(0)
+            frames.append(torch.from_numpy(to_float(u8)).unsqueeze(0))
+    else:
+        meta["frame_sha256"] = [digest(x) for x in frames]
+    with torch.no_grad():
+        dpb = None
+        for t in range(nframes if write_frames is None else write_frames):
+            x = frames[t]
             xp = pad64(x)
             if t == 0:
                 qs, qidx = round(qi * 100) / 100, round(qi * 100)
@@ -189,7 +197,7 @@ def run_sequence(DMC, IntraNoAR, i_sd, p_sd, h, w, nframes, q, seed, out, tag):
             meta["write"].append(entry)
         dpb = None
         for t in range(nframes):
-            x = torch.from_numpy(to_float(out[f"{tag}_frame{t}"])).unsqueeze(0)
+            x = frames[t]
             xp = pad64(x)
             if t == 0:
                 r = inet.encode_decode(xp, qi, None, pic_height=h, pic_width=w)
@@ -221,6 +229,15 @@ def main():
     out, meta = {}, {}
     meta["A"] = run_sequence(DMC, IntraNoAR, i_sd, p_sd, 128, 192, 3, (1.08, 1.10, 0.96), 1, out, "A")
     meta["B"] = run_sequence(DMC, IntraNoAR, i_sd, p_sd, 100, 150, 3, (0.73, 1.01, 0.71), 2, out, "B")
+    # config C1 (BASELINE.json configs[0]): 4 random 256x256 frames, IP=4
+    # (I P P P), estimate mode on all four, write mode on I, P1, P2 (the survey's
+    # recipe); q scales = rate 0 of the weights' ladders
+    g = torch.Generator().manual_seed(1)
+    c1_frames = [torch.rand(1, 3, 256, 256, generator=g) for _ in range(4)]
+    c1_q = (float(i_sd["q_scale"].reshape(-1)[0]), float(p_sd["mv_y_q_scale"].reshape(-1)[0]),
+            float(p_sd["y_q_scale"].reshape(-1)[0]))
+    meta["C1"] = run_sequence(DMC, IntraNoAR, i_sd, p_sd, 256, 256, 4, c1_q, 1, out, "C1",
+                              frames=c1_frames, write_frames=3)
     np.savez_compressed(os.path.join(HERE, "hem_golden.npz"), **out)
     with open(os.path.join(HERE, "hem_golden.json"), "w") as f:
         json.dump(meta, f, indent=1)

@@ -34,12 +34,19 @@ class HEMGolden:
         return z[f"table_{name}_cdf"], z[f"table_{name}_len"], z[f"table_{name}_off"]
 
     def frame_tensor(self, tag, t):
-        """Frame padded with zeros to a multiple of 64 (HEM test_video.py:113-119)."""
-        u8 = self.npz[f"{tag}_frame{t}"]
-        x = torch.from_numpy(to_float(u8)).unsqueeze(0)
-        h, w = u8.shape[1:]
+        """Frame padded with zeros to a multiple of 64 (HEM test_video.py:113-119).
+        Config C1's frames are torch.rand draws (make_golden_hem.py), rebuilt here."""
+        if "frame_sha256" in self.meta[tag]:
+            g = torch.Generator().manual_seed(1)
+            x = [torch.rand(1, 3, self.meta[tag]["h"], self.meta[tag]["w"], generator=g) for _ in range(t + 1)][t]
+        else:
+            x = torch.from_numpy(to_float(self.npz[f"{tag}_frame{t}"])).unsqueeze(0)
+        h, w = x.shape[2:]
         xp = torch.nn.functional.pad(x, (0, (64 - w % 64) % 64, 0, (64 - h % 64) % 64), mode="constant", value=0)
         return x, xp
+
+    def write_frames(self, tag):
+        return len(self.meta[tag]["write"])
 
     def calls(self, tag, t):
         e = self.meta[tag]["write"][t]

@@ -314,6 +314,39 @@ def test_gemm1x1_equals_generic_conv(case, xdt):
     assert rel_err(back(y), ref) < 2e-2
 
 
+@pytest.mark.parametrize("case", [(384, 384, 68, 120), (1024, 384, 17, 30), (384, 1024, 9, 13), (192, 192, 68, 120),
+                                  (768, 192, 20, 33), (40, 64, 17, 19), (128, 512, 33, 47), (96, 288, 34, 60),
+                                  (64, 2, 8, 9), (104, 16, 5, 7)])
+def test_gemm1x1_f32_equals_generic_conv(case):
+    """The fp32 1x1 GEMM (gemm1x1f.hip) and conv.hip's f32 path run the same
+    exact-f32 MFMA chain (k ascending, 4 per instruction): bit-identical
+    outputs with the lrelu input op, activation, residual and shuffle; and
+    within f32 tolerance of torch."""
+    h = K()
+    cin, cout, H, W = case
+    x = torch.randn(1, cin, H, W)
+    w = torch.randn(cout, cin, 1, 1) / cin ** 0.5
+    b = torch.randn(cout) * 0.1
+    cw = h.ConvW(w, b, 1, h.F32)
+    xa = to_act(x, h.F32)
+    rt = torch.randn(1, cout, H, W)
+    outs = []
+    for use in (1, 0):
+        h.set_option("gemm1x1_f32", use)
+        r = to_act(rt, h.F32)
+        y = h.conv(cw, xa, out_dtype=h.F32, in_op=h.IN_LRELU, in_slope=0.1, act=h.ACT_LRELU, slope=0.01, res=r)
+        y1 = h.conv(cw, xa, out_dtype=h.F32)
+        y2 = h.conv(cw, xa, shuffle=True, out_dtype=h.F32) if cout % 4 == 0 else y1
+        torch.cuda.synchronize()
+        outs.append((back(y), back(y1), back(y2)))
+    h.set_option("gemm1x1_f32", 1)
+    for a, c in zip(outs[0], outs[1]):
+        assert torch.equal(a, c)
+    ref = F.leaky_relu(F.conv2d(F.leaky_relu(x, 0.1), w, b), 0.01) + rt
+    assert rel_err(outs[0][0], ref) < 2e-5
+    assert rel_err(outs[0][1], F.conv2d(x, w, b)) < 2e-5
+
+
 C3_CASES = [
     # cin, cout, H, W, coff (input channel view offset in a wider buffer)
     (64, 64, 37, 61, 0), (96, 192, 20, 33, 0), (128, 128, 9, 13, 0), (192, 96, 11, 70, 0),

@@ -63,12 +63,12 @@ def oracle_runs(hem_golden):
     tables = {n: hem_golden.table(n) for n in ("i_y", "i_z", "p_y", "p_z", "p_mvz")}
     runs = {}
     with torch.no_grad():
-        for tag in ("A", "B"):
+        for tag in ("A", "B", "C1"):
             meta = hem_golden.meta[tag]
             qi, qmv, qy = hem_golden.q(tag)
             h, w = meta["h"], meta["w"]
             frames, dpb = [], None
-            for t in range(meta["frames"]):
+            for t in range(hem_golden.write_frames(tag)):
                 x, _ = hem_golden.frame_tensor(tag, t)
                 calls = hem_golden.calls(tag, t)
                 pos = [0]
@@ -100,7 +100,7 @@ def run_product(g, tag, prec, estimate=False):
     pnet.update(force=True)
     out, dpb = [], None
     with tempfile.TemporaryDirectory() as td:
-        for t in range(meta["frames"]):
+        for t in range(meta["frames"] if estimate else g.write_frames(tag)):
             x, xp = g.frame_tensor(tag, t)
             xp = xp.cuda()
             net = inet if t == 0 else pnet
@@ -142,8 +142,13 @@ def check(stats, tol):
         assert abs(s["psnr"] - s["psnr_oracle"]) <= tol["psnr_db"], s
 
 
-@pytest.mark.parametrize("mode", ["parity", "fast"])
-@pytest.mark.parametrize("tag", ["A", "B"])
+# C1's random frames and wider latents move HEM symbols across rounding ties
+# more often; a tie flipped in one frame changes that frame's y_hat and with it
+# every later frame of a free-running sequence, so C1 parity is checked per
+# frame on the reference's own dpb (teacher-forced) in
+# tests/test_gpu_parity_strict.py; free-running C1 runs in fast mode here.
+@pytest.mark.parametrize("mode,tag", [("parity", "A"), ("parity", "B"), ("fast", "A"), ("fast", "B"),
+                                      ("fast", "C1")])
 def test_hem_write_mode_vs_reference(hem_golden, oracle_runs, tag, mode):
     from dcvc_amd.layers import Precision
     prec = Precision.parity() if mode == "parity" else Precision.fast()
@@ -152,8 +157,8 @@ def test_hem_write_mode_vs_reference(hem_golden, oracle_runs, tag, mode):
     check(stats, PARITY_TOL if mode == "parity" else HEM_FAST_TOL)
 
 
-@pytest.mark.parametrize("mode", ["parity", "fast"])
-@pytest.mark.parametrize("tag", ["A", "B"])
+@pytest.mark.parametrize("mode,tag", [("parity", "A"), ("parity", "B"), ("fast", "A"), ("fast", "B"),
+                                      ("fast", "C1")])
 def test_hem_estimate_mode_vs_reference(hem_golden, tag, mode):
     from dcvc_amd.layers import Precision
     prec = Precision.parity() if mode == "parity" else Precision.fast()

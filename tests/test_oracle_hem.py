@@ -42,7 +42,7 @@ def _indexes(oracle, kind, sym, scales):
     return O.build_indexes(scales, oracle.tab_y[3], oracle.tab_y[4]).reshape(-1)
 
 
-@pytest.mark.parametrize("tag", ["A", "B"])
+@pytest.mark.parametrize("tag", ["A", "B", "C1"])
 def test_write_mode_matches_reference(hem_golden, oracles, tag):
     i, p = oracles
     meta = hem_golden.meta[tag]
@@ -50,7 +50,7 @@ def test_write_mode_matches_reference(hem_golden, oracles, tag):
     h, w = meta["h"], meta["w"]
     dpb = None
     with torch.no_grad():
-        for t in range(meta["frames"]):
+        for t in range(hem_golden.write_frames(tag)):
             _, xp = hem_golden.frame_tensor(tag, t)
             ref_calls = hem_golden.calls(tag, t)
             if t == 0:
@@ -82,7 +82,13 @@ def test_write_mode_matches_reference(hem_golden, oracles, tag):
                     assert digest(dpb[k]) == e[k + "_sha256"], f"{tag} t={t} {k}"
 
 
-@pytest.mark.parametrize("tag", ["A", "B"])
+def test_c1_frames(hem_golden):
+    for t in range(hem_golden.meta["C1"]["frames"]):
+        x, _ = hem_golden.frame_tensor("C1", t)
+        assert digest(x) == hem_golden.meta["C1"]["frame_sha256"][t]
+
+
+@pytest.mark.parametrize("tag", ["A", "B", "C1"])
 def test_estimate_mode_matches_reference(hem_golden, oracles, tag):
     i, p = oracles
     meta = hem_golden.meta[tag]

@@ -63,7 +63,7 @@ def symbols(n, ntab, seed, wide=False, negative_idx=False):
     return s, idx
 
 
-@pytest.mark.parametrize("parts", [1, 2, 4])
+@pytest.mark.parametrize("parts", [1, 2, 4, 8, 16])
 @pytest.mark.parametrize("mt", [False, True])
 def test_dc_stream_byte_exact_vs_oracle_and_roundtrip(parts, mt):
     tab = laplace_table()
