@@ -6,6 +6,7 @@
 #   oracle/_ref/                  test-only build of the reference's own
 #                                  ops.cpp (only when /root/reference exists)
 HIPCC    ?= /opt/rocm/bin/hipcc
+HIPFLAGS ?= -fno-slp-vectorize
 CXX      ?= g++
 CC       ?= gcc
 ARCH     ?= gfx950
@@ -33,7 +34,7 @@ $(LIB)/libdcvc_rans.so: dcvc_amd/csrc/rans/dcvc_rans.cpp include/dcvc_rans.h
 
 build/hip/%.o: dcvc_amd/csrc/hip/%.hip $(HIP_HDRS)
 	@mkdir -p build/hip
-	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall -c -o $@ $<
+	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall $(HIPFLAGS) -c -o $@ $<
 
 $(LIB)/libdcvc_hip.so: $(HIP_OBJS)
 	@mkdir -p $(LIB)

@@ -209,10 +209,11 @@ int launch(GF p, hipStream_t st) {
 int g_use_gemm_f32 = 1;
 int g_cfg = 0;  // dcvc_set_option("gemm1x1_f32_cfg", i): force tile config i (A/B), 0 = automatic
 
-// Tile choice: the widest BN in {128, 64, 32} whose grid still has >= 512
-// workgroups at BM = 64 (two per CU or more: the f32 MFMA loop is long, so
-// fewer, fuller tiles win while every CU has work); narrower maps fall back
-// to 32-pixel tiles.
+// Tile choice, from A/B timings of every configuration on the 68x120 latent
+// shapes (scripts/gemm_f32_bench.py, profiles/r02_gemm_f32.jsonl): 64 x 64
+// tiles with 32-channel steps for Cout >= 256, 64 x 32 tiles with 64-channel
+// steps below (1.2-1.8x over the widest-tile rule at 384->1024, 768->192,
+// 512->128); maps too small to give 512 such workgroups use 32-pixel tiles.
 int dispatch(const GF &p, hipStream_t st) {
   switch (g_cfg) {
     case 1: return launch<64, 64, 2, 32>(p, st);
@@ -229,9 +230,8 @@ int dispatch(const GF &p, hipStream_t st) {
     default: break;
   }
   auto blocks = [&](int bm, int bn) { return (long)((p.M + bm - 1) / bm) * ((p.cout + bn - 1) / bn); };
-  if (p.cout > 64 && blocks(64, 128) >= 512) return launch<64, 128, 2, 32>(p, st);
-  if (p.cout > 32 && blocks(64, 64) >= 512) return launch<64, 64, 2, 32>(p, st);
-  if (blocks(64, 32) >= 512) return launch<64, 32, 4, 32>(p, st);
+  if (p.cout >= 256 && blocks(64, 64) >= 512) return launch<64, 64, 2, 32>(p, st);
+  if (blocks(64, 32) >= 512) return launch<64, 32, 4, 64>(p, st);
   if (p.cout > 32) return launch<32, 64, 2, 32>(p, st);
   return launch<32, 32, 2, 32>(p, st);
 }

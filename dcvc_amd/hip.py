@@ -251,10 +251,28 @@ CANARY = None
 _CANARY_BYTES = 4096
 
 
+# Debug aid (DCVC_POISON=nan|rand): every K.empty activation starts as NaN or
+# as random bits (different per allocation) instead of whatever the caching
+# allocator hands back, so a kernel that reads elements nobody wrote shows up
+# as NaN or as an encoder/decoder divergence.
+POISON = os.environ.get("DCVC_POISON", "")
+
+
+def _poison(t):
+    if POISON == "nan":
+        t.view(torch.int16 if t.element_size() == 2 else torch.int32).fill_(-1)
+    elif POISON == "rand":
+        v = t.view(torch.int16 if t.element_size() == 2 else torch.int32)
+        v.random_(-(1 << 15) if t.element_size() == 2 else -(1 << 31), (1 << 15) if t.element_size() == 2 else (1 << 31))
+    return t
+
+
 def _alloc(H, W, C, dtype, dev, zero):
     if CANARY is None:
-        f = torch.zeros if zero else torch.empty
-        return Act(f((H, W, C), dtype=_TORCH[dtype], device=dev))
+        if zero:
+            return Act(torch.zeros((H, W, C), dtype=_TORCH[dtype], device=dev))
+        t = torch.empty((H, W, C), dtype=_TORCH[dtype], device=dev)
+        return Act(_poison(t) if POISON else t)
     import traceback
     n = H * W * C
     es = 4 if dtype == F32 else 2
