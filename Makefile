@@ -6,6 +6,8 @@
 #   oracle/_ref/                  test-only build of the reference's own
 #                                  ops.cpp (only when /root/reference exists)
 HIPCC    ?= /opt/rocm/bin/hipcc
+# -fno-slp-vectorize: no packed-f32 VALU instructions in the kernels
+# (scripts/check_isa.sh explains why and enforces it)
 HIPFLAGS ?= -fno-slp-vectorize
 CXX      ?= g++
 CC       ?= gcc
@@ -36,9 +38,10 @@ build/hip/%.o: dcvc_amd/csrc/hip/%.hip $(HIP_HDRS)
 	@mkdir -p build/hip
 	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall $(HIPFLAGS) -c -o $@ $<
 
-$(LIB)/libdcvc_hip.so: $(HIP_OBJS)
+$(LIB)/libdcvc_hip.so: $(HIP_OBJS) scripts/check_isa.sh
 	@mkdir -p $(LIB)
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^
+	bash scripts/check_isa.sh $(HIP_OBJS)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(HIP_OBJS)
 
 oracle/_build/liboracle_rans.so: oracle/rans_oracle.c
 	@mkdir -p oracle/_build

@@ -52,9 +52,10 @@ def parse():
                          "end to end; fast-bf16-tail = bf16 MFMA for the entropy-parameter tail too (labelled)")
     ap.add_argument("--stream_part", type=int, default=8,
                     help="rANS stream parts (the reference's --stream_part_i/p); parts code in parallel threads")
-    ap.add_argument("--lanes", type=int, default=1, choices=[1],
-                    help="GOP lanes per GPU.  Concurrent lanes (separate HIP streams / processes sharing the GPU) "
-                         "are disabled: co-running codecs showed an encoder/decoder divergence (DESIGN.md §9)")
+    ap.add_argument("--lanes", type=int, default=3,
+                    help="GOP lanes per GPU: independent GOPs coded concurrently by host threads on their own HIP "
+                         "streams (the reference's several workers per GPU, test_video.py:289-290), so one lane's "
+                         "host rANS work overlaps another's kernels")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16,
                     help="host threads for the cpu_baseline oracle run (capped at the cores this process may use)")
@@ -340,9 +341,8 @@ def main():
         """One GOP lane: its own codec instances, HIP stream, frame staging
         and output folder.  Lane l codes GOP l of this rank's sequence (an
         I-frame resets the DPB, so GOPs are independent, test_video.py:
-        140-150).  One lane per GPU: concurrent lanes (meant to overlap one
-        lane's host rANS work with another's kernels) are disabled until the
-        co-running divergence of DESIGN.md §9 is resolved."""
+        140-150).  With several lanes each runs on its own host thread and
+        HIP stream, so one lane's host rANS work overlaps another's kernels."""
 
         def __init__(self, l):
             self.l = l
@@ -354,7 +354,7 @@ def main():
                 self.pnet = DMC(precision=prec, stream_part=args.stream_part, device=device).load_state_dict(psd)
             self.inet.update(force=True)
             self.pnet.update(force=True)
-            self.stream = torch.cuda.current_stream(device)
+            self.stream = torch.cuda.Stream(device) if args.lanes > 1 else torch.cuda.current_stream(device)
             # run_test's frame handling (dcvc_amd.harness.FrameStage): uint8
             # source resident in HBM, converted to the padded NHWC input
             # inside the step; the distortion (in-place clamp + squared-error
@@ -416,8 +416,24 @@ def main():
     torch.cuda.synchronize(device)   # setup work on the default stream is done before lanes start
 
     def run_all(idx, timed):
-        for ln in lanes:
-            ln.run(idx, timed)
+        if len(lanes) == 1:
+            lanes[0].run(idx, timed)
+            return
+        import threading
+        errs = []
+
+        def go(ln):
+            try:
+                ln.run(idx, timed)
+            except BaseException as e:  # noqa: BLE001 - re-raised on the main thread
+                errs.append(e)
+        th = [threading.Thread(target=go, args=(ln,)) for ln in lanes]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        if errs:
+            raise errs[0]
 
     run_all(warm_idx, False)
     torch.cuda.synchronize(device)

@@ -1,0 +1,29 @@
+#!/bin/bash
+# Build-time ISA check of libdcvc_hip's gfx950 code objects.
+#
+# The kernels must not contain packed-f32 VALU instructions (v_pk_mul_f32,
+# v_pk_add_f32, v_pk_fma_f32): with them, kernels of a codec that shares the
+# GPU with another process (or with another stream's work on a second
+# hardware queue) intermittently produced wrong values in the low lane of
+# packed results (the co-running divergence), while the same
+# build without them ran clean.  The Makefile builds with -fno-slp-vectorize,
+# which keeps the compiler from forming them; this check fails the build if
+# any appear (a new source using packed math explicitly, or a flag change).
+#   scripts/check_isa.sh build/hip/*.o
+set -eu
+B=/opt/rocm/lib/llvm/bin
+T=$(mktemp -d)
+trap 'rm -rf "$T"' EXIT
+bad=0
+for o in "$@"; do
+  n=$(basename "$o" .o)
+  "$B/llvm-objcopy" --dump-section .hip_fatbin="$T/$n.fat" "$o"
+  "$B/clang-offload-bundler" --unbundle --type=o --targets=hipv4-amdgcn-amd-amdhsa--gfx950 \
+    --input="$T/$n.fat" --output="$T/$n.co"
+  c=$("$B/llvm-objdump" -d "$T/$n.co" | grep -cE "v_pk_(mul|add|fma)_f32" || true)
+  if [ "$c" != "0" ]; then
+    echo "check_isa: $o has $c packed-f32 instructions" >&2
+    bad=1
+  fi
+done
+exit $bad
