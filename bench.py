@@ -558,7 +558,8 @@ def main():
                        "ms_P": round(1e3 * float(np.mean(tp)), 2) if tp else None,
                        "timed_frames": [timed_idx[0], timed_idx[-1]],
                        **({"fps_gop_avg": round(args.gop / (float(np.mean(ti)) + (args.gop - 1) * float(np.mean(tp))),
-                                                 3)} if ti and tp else {}),
+                                                 3)} if ti and tp and args.lanes == 1 else {}),
+                       "step": f"one frame on each of {args.lanes} lane(s)",
                        "bpp": round(float(np.mean(timed_bits)) / (h * w), 5), **psnr,
                        **({"bits_per_lane": [int(sum(ln.bits[i] for i in timed_idx)) for ln in lanes]}
                           if args.lanes > 1 else {})},

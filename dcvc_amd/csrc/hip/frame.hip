@@ -142,6 +142,47 @@ __global__ void __launch_bounds__(SSE_BLOCK) sse_yuv420_kernel(FView xh, const u
   block_sum3(a[0], a[1], a[2], part);
 }
 
+__device__ __forceinline__ uint8_t q255(float v) {
+  return (uint8_t)fminf(fmaxf(rintf(v * 255.f), 0.f), 255.f);  // np.clip(np.rint(v * 255), 0, 255)
+}
+
+// dcvc_recon_to_u8, RGB: one thread per crop pixel, HWC uint8
+__global__ void recon_rgb_u8_kernel(FView xh, int h, int w, uint8_t *out) {
+  const int64_t pix = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (pix >= (int64_t)h * w) return;
+  const int py = (int)(pix / w), px = (int)(pix - (int64_t)py * w);
+  const float *p = xh.p + ((int64_t)py * xh.W + px) * xh.cs + xh.co;
+#pragma unroll
+  for (int c = 0; c < 3; ++c) out[pix * 3 + c] = q255(p[c]);
+}
+
+// dcvc_recon_to_u8, YUV420: one thread per 2x2 block of the crop; Y of the
+// four pixels and the block's U, V means, ycbcr444_to_420 of the values as
+// given (clip after the mean; run_test hands over the frame already clamped)
+// with sse_yuv420_kernel's summation order
+__global__ void recon_yuv_u8_kernel(FView xh, int h, int w, uint8_t *out) {
+  const int hh = h / 2, hw = w / 2;
+  const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= (int64_t)hh * hw) return;
+  const int by = (int)(b / hw), bx = (int)(b - (int64_t)by * hw);
+  float s[3] = {0.f, 0.f, 0.f};
+  float v[2][2][3];
+#pragma unroll
+  for (int dy = 0; dy < 2; ++dy)
+#pragma unroll
+    for (int dx = 0; dx < 2; ++dx) {
+      const float *p = xh.p + ((int64_t)(2 * by + dy) * xh.W + 2 * bx + dx) * xh.cs + xh.co;
+#pragma unroll
+      for (int c = 0; c < 3; ++c) v[dy][dx][c] = p[c];
+      out[(int64_t)(2 * by + dy) * w + 2 * bx + dx] = q255(clamp01(v[dy][dx][0]));
+    }
+#pragma unroll
+  for (int c = 1; c < 3; ++c) {
+    s[c] = (v[0][0][c] + v[0][1][c]) + (v[1][0][c] + v[1][1][c]);
+    out[(int64_t)h * w + (int64_t)(c - 1) * hh * hw + b] = q255(clamp01(s[c] / 4.f));
+  }
+}
+
 // Fixed-order final reduction of the per-block partials: out[c] = sum_b part[3b + c].
 __global__ void __launch_bounds__(256) sse_final_kernel(const double *part, int nb, double *out) {
   __shared__ double red[4][3];
@@ -202,6 +243,19 @@ extern "C" int dcvc_frame_sse(dcvc_tensor x_hat, const uint8_t *src, const uint8
   }
   DCVC_LAUNCH_CHECK();
   hipLaunchKernelGGL(sse_final_kernel, dim3(1), dim3(256), 0, st, workspace, (int)g, out3);
+  DCVC_LAUNCH_CHECK();
+  return DCVC_HIP_OK;
+}
+
+extern "C" int dcvc_recon_to_u8(dcvc_tensor x_hat, int h, int w, int yuv420, uint8_t *out, void *stream) {
+  if (!frame_ok(x_hat) || !out || h <= 0 || w <= 0 || x_hat.H < h || x_hat.W < w) return DCVC_HIP_EINVAL;
+  if (yuv420 && ((h & 1) || (w & 1))) return DCVC_HIP_EINVAL;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int64_t n = yuv420 ? (int64_t)(h / 2) * (w / 2) : (int64_t)h * w;
+  if (yuv420)
+    hipLaunchKernelGGL(recon_yuv_u8_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, fv(x_hat), h, w, out);
+  else
+    hipLaunchKernelGGL(recon_rgb_u8_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, fv(x_hat), h, w, out);
   DCVC_LAUNCH_CHECK();
   return DCVC_HIP_OK;
 }

@@ -284,6 +284,107 @@ class MsSsimRGB:
         return res
 
 
+class ReconWriter:
+    """--save_decoded_frame: PNGWriter (im00001.png, ...) and YUVWriter
+    (out.yuv) of DCVC-DC/src/utils/video_writer.py:26-111 as test_video.py:
+    84-88, 210-221 drives them, and DCVC-HEM's save_torch_image
+    ({frame_idx}.png, DCVC-HEM/test_video.py:68-71, 161-163).
+
+    The decoded frame is quantised on the GPU (dcvc_recon_to_u8: the crop,
+    clip(rint(v * 255)), and for YUV the ycbcr444_to_420 chroma means), copied
+    once to pinned memory, and written by one background thread in frame order
+    so file encoding overlaps the next frame.  kind: "png" | "yuv" | "hem_png";
+    src_format "rgb" | "420" (what the codec's frames hold, dist_in_yuv420).
+    The reference's cross cases (a 4:2:0 frame into PNGWriter, an RGB frame into
+    YUVWriter) convert on the host with its own formulas
+    (functional.py:16-58)."""
+
+    def __init__(self, path, h, w, kind, src_format, device):
+        from concurrent.futures import ThreadPoolExecutor
+        os.makedirs(path, exist_ok=True)
+        self.path, self.h, self.w, self.kind, self.fmt = path, h, w, kind, src_format
+        self.yuv_out = kind == "yuv"
+        quant_yuv = src_format == "420"
+        self.quant_yuv = quant_yuv
+        self.n = h * w + 2 * (h // 2) * (w // 2) if quant_yuv else 3 * h * w
+        self.dev_buf = torch.empty(self.n, dtype=torch.uint8, device=device)
+        self.pool = ThreadPoolExecutor(1)
+        self.jobs = []
+        self.index = 1                              # PNGWriter.current_frame_index starts at 1
+        self.file = open(os.path.join(path, "out.yuv"), "wb") if self.yuv_out else None
+
+    def write(self, recon, frame_idx):
+        from .dc.video_model import as_act
+        x = as_act(recon)
+        if (self.fmt == "rgb") == self.yuv_out:
+            # the cross cases: the float frame to the host, the reference's conversion there
+            f = x.t()[:self.h, :self.w].float().permute(2, 0, 1).cpu().numpy()
+            if self.yuv_out:
+                self.jobs.append(self.pool.submit(self._yuv_from_rgb, f))
+            else:
+                name = f"im{str(self.index).zfill(5)}.png"
+                self.index += 1
+                self.jobs.append(self.pool.submit(self._png_from_444, f, name))
+            return
+        K.recon_to_u8(x, self.h, self.w, self.quant_yuv, self.dev_buf)
+        host = torch.empty(self.n, dtype=torch.uint8, pin_memory=True)
+        host.copy_(self.dev_buf, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        name = (f"im{str(self.index).zfill(5)}.png" if self.kind == "png" else f"{frame_idx}.png")
+        self.index += 1
+        self.jobs.append(self.pool.submit(self._emit, host, ev, name))
+
+    def _emit(self, host, ev, name):
+        ev.synchronize()
+        a = host.numpy()
+        h, w = self.h, self.w
+        if self.yuv_out:
+            self.file.write(a.tobytes())            # Y plane then U, V planes (YUVWriter)
+            return
+        from PIL import Image
+        Image.fromarray(a.reshape(h, w, 3)).save(os.path.join(self.path, name))
+
+    def _png_from_444(self, yuv, name):
+        # 4:2:0 frame into PNGWriter: ycbcr444_to_420 (y_rec, uv_rec as test_video.py:170-171 forms them),
+        # then ycbcr420_to_rgb(order=1) and the PNG quantisation (functional.py:42-58, video_writer.py:34-45)
+        import scipy.ndimage
+        from PIL import Image
+        h, w = self.h, self.w
+        y = np.clip(yuv[0:1], 0.0, 1.0)
+        u = np.mean(np.reshape(yuv[1:2], (1, h // 2, 2, w // 2, 2)), axis=(-1, -3))
+        v = np.mean(np.reshape(yuv[2:3], (1, h // 2, 2, w // 2, 2)), axis=(-1, -3))
+        uv = scipy.ndimage.zoom(np.clip(np.concatenate((u, v), axis=0), 0.0, 1.0), (1, 2, 2), order=1)
+        kr, kg, kb = 0.2126, 0.7152, 0.0722
+        r = y + (2 - 2 * kr) * (uv[1:2] - 0.5)
+        b = y + (2 - 2 * kb) * (uv[0:1] - 0.5)
+        g = (y - kr * r - kb * b) / kg
+        rgb = np.clip(np.concatenate((r, g, b), 0), 0.0, 1.0).transpose(1, 2, 0)
+        Image.fromarray(np.clip(np.rint(rgb * 255), 0, 255).astype(np.uint8)).save(os.path.join(self.path, name))
+
+    def _yuv_from_rgb(self, rgb):
+        r, g, b = np.split(rgb, 3, axis=0)
+        kr, kg, kb = 0.2126, 0.7152, 0.0722
+        y = kr * r + kg * g + kb * b
+        cb = 0.5 * (b - y) / (1 - kb) + 0.5
+        cr = 0.5 * (r - y) / (1 - kr) + 0.5
+        h, w = self.h, self.w
+        cb = np.mean(np.reshape(cb, (1, h // 2, 2, w // 2, 2)), axis=(-1, -3))
+        cr = np.mean(np.reshape(cr, (1, h // 2, 2, w // 2, 2)), axis=(-1, -3))
+        uv = np.clip(np.concatenate((cb, cr), axis=0), 0.0, 1.0)
+        y = np.clip(y, 0.0, 1.0)
+        self.file.write(np.clip(np.rint(y * 255), 0, 255).astype(np.uint8).tobytes())
+        self.file.write(np.clip(np.rint(uv * 255), 0, 255).astype(np.uint8).tobytes())
+
+    def close(self):
+        for j in self.jobs:
+            j.result()
+        self.jobs = []
+        self.pool.shutdown()
+        if self.file is not None:
+            self.file.close()
+
+
 def psnr_rgb(sse3, h, w):
     """PSNR() of test_video.py:65-68: mse = mean((x_hat - x)^2) as an fp32
     tensor, psnr = 20 * log10(1 / sqrt(mse)) in fp32."""
@@ -393,8 +494,6 @@ def run_test(p_frame_net, i_frame_net, args):
     frame_num, gop_size = args["frame_num"], args["gop_size"]
     write_stream = bool(args.get("write_stream", False))
     verbose = args.get("verbose", 0)
-    if args.get("save_decoded_frame"):
-        raise NotImplementedError("save_decoded_frame: the video writers are out of scope (DESIGN.md §10)")
     yuv = bool(args.get("dist_in_yuv420", False))
     if yuv and args.get("src_type", "yuv420") != "yuv420" and "src_reader" not in args:
         raise ValueError("dist_in_yuv420 needs a yuv420 source")
@@ -402,6 +501,10 @@ def run_test(p_frame_net, i_frame_net, args):
     reader = _reader(args, yuv)
     h, w = args["src_height"], args["src_width"]
     stage = FrameStage(h, w, 16, yuv, zero_pad=False, frame_num=frame_num, device=device)
+    writer = None
+    if args.get("save_decoded_frame"):   # test_video.py:84-88
+        writer = ReconWriter(args["recon_path"], h, w, "png" if args.get("src_type", "yuv420") == "png" else "yuv",
+                             "420" if yuv else "rgb", device)
     ms = None
     if args.get("calc_ssim"):
         ms = MsSsim(h, w, frame_num, device) if yuv else MsSsimRGB(h, w, frame_num, device)
@@ -443,8 +546,12 @@ def run_test(p_frame_net, i_frame_net, args):
                     ms.run(as_act(recon), dframe[0], dframe[1], frame_idx)
                 else:
                     ms.run(as_act(recon), dframe, frame_idx)
+            if writer is not None:
+                writer.write(recon, frame_idx)
             if verbose >= 2:
                 print(f"frame {frame_idx}, bits: {bits[-1]:.3f}", flush=True)
+    if writer is not None:
+        writer.close()
     sse = stage.sums()
     test_time = time.time() - start_time
     if verbose >= 1 and p_frame_number > 0:
@@ -465,6 +572,12 @@ def run_test(p_frame_net, i_frame_net, args):
                                 verbose=verbose >= 1)
     if args.get("calc_ssim") and not yuv:
         log["msssim_unpinned"] = True   # pytorch_msssim's algorithm, package absent (MsSsimRGB)
+    if writer is not None:
+        # test_video.py:217-221: the recon folder is renamed after the rate point's averages
+        avg_bpp = sum(bits) / len(bits) / w / h
+        avg_psnr = log["ave_all_frame_psnr"]
+        folder = f"{args.get('rate_idx', 0)}_{avg_bpp:.4f}_{avg_psnr:.4f}"
+        os.rename(args["recon_path"], args["recon_path"] + f"/../{folder}")
     return log
 
 
@@ -484,13 +597,14 @@ def run_test_hem(video_net, i_frame_net, args, device=None):
     p_frame_mv_y_q_scale, p_frame_y_q_scale)."""
     frame_num, gop_size = args["frame_num"], args["gop_size"]
     write_stream = bool(args.get("write_stream", False))
-    if args.get("save_decoded_frame"):
-        raise NotImplementedError("save_decoded_frame: the PNG writer is out of scope (DESIGN.md §10)")
     device = device if device is not None else i_frame_net.dev
     reader = _reader({**args, "src_type": args.get("src_type", "png")}, False)
     h, w = args["src_height"], args["src_width"]
     stage = FrameStage(h, w, 64, False, zero_pad=True, frame_num=frame_num, device=device)
     ms = MsSsimRGB(h, w, frame_num, device) if min(h, w) > 160 else None  # HEM always reports ms_ssim (:150)
+    writer = None
+    if args.get("save_decoded_frame"):   # DCVC-HEM/test_video.py:161-163, 204-209
+        writer = ReconWriter(args["decoded_frame_folder"], h, w, "hem_png", "rgb", device)
     frame_types, bits = [], []
     start_time = time.time()
     dpb = None
@@ -519,6 +633,10 @@ def run_test_hem(video_net, i_frame_net, args, device=None):
             if ms is not None:
                 from .dc.video_model import as_act
                 ms.run(as_act(recon), dframe, frame_idx)
+            if writer is not None:
+                writer.write(recon, frame_idx)
+    if writer is not None:
+        writer.close()
     sse = stage.sums()
     psnrs = [psnr_rgb(sse[i], h, w) for i in range(frame_num)]
     mv = ms.values(frame_num) if ms is not None else [0.0] * frame_num

@@ -70,6 +70,7 @@ HIP_SYMBOLS = [
     ("dcvc_yuv420_to_nhwc", _i, [_vp, _vp, _i, _i, _T, _vp]),
     ("dcvc_frame_sse_workspace", ctypes.c_int64, []),
     ("dcvc_frame_sse", _i, [_T, _vp, _vp, _i, _i, _i, _vp, _vp, _vp]),
+    ("dcvc_recon_to_u8", _i, [_T, _i, _i, _i, _vp, _vp]),
     ("dcvc_quadtree_encode_step", _i, [_T, _T, _T, _i, _T, _T, _vp, _vp, _f, _f, _vp]),
     ("dcvc_quadtree_indexes_step", _i, [_T, _T, _i, _vp, _f, _f, _vp]),
     ("dcvc_quadtree_decode_step", _i, [_T, _T, _i, _vp, _T, _T, _vp]),
@@ -500,6 +501,15 @@ def frame_sse(x_hat, src_u8, h, w, workspace, out3, uv_u8=None):
     check(lib().dcvc_frame_sse(x_hat.c(), src_u8.data_ptr(), uv_u8.data_ptr() if yuv else None, h, w, int(yuv),
                                workspace.data_ptr(), out3.data_ptr(), stream()), "frame_sse")
     return out3
+
+
+def recon_to_u8(x_hat, h, w, yuv420, out):
+    """Decoded frame -> uint8 as the --save_decoded_frame writers store it
+    (dcvc_recon_to_u8): HWC RGB, or Y | U | V planes."""
+    n = h * w + 2 * (h // 2) * (w // 2) if yuv420 else 3 * h * w
+    assert out.dtype == torch.uint8 and out.numel() >= n and x_hat.dtype == F32 and x_hat.C == 3
+    check(lib().dcvc_recon_to_u8(x_hat.c(), h, w, 1 if yuv420 else 0, out.data_ptr(), stream()), "recon_to_u8")
+    return out
 
 
 def yuv_planes_f64(x_hat, y_u8, uv_u8, h, w, src, rec):

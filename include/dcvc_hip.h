@@ -193,6 +193,15 @@ int64_t dcvc_frame_sse_workspace(void);
 int dcvc_frame_sse(dcvc_tensor x_hat, const uint8_t *src, const uint8_t *uv,
                    int h, int w, int yuv420, double *workspace, double *out3,
                    void *stream);
+/* The decoded frame as run_test's --save_decoded_frame writers store it
+ * (DCVC-DC/src/utils/video_writer.py:26-111, DCVC-HEM/test_video.py:68-71):
+ * the top-left h x w crop of x_hat (fp32 NHWC, 3 ch) quantised as
+ * clip(rint(v * 255), 0, 255) in fp32, into out (device uint8):
+ *   yuv420 = 0: h x w x 3 interleaved (PNGWriter / save_torch_image);
+ *   yuv420 = 1: Y plane (h x w) then U, V planes (h/2 x w/2) of
+ *               ycbcr444_to_420(clip(x_hat)) (YUVWriter), h and w even. */
+int dcvc_recon_to_u8(dcvc_tensor x_hat, int h, int w, int yuv420, uint8_t *out,
+                     void *stream);
 
 /*
  * Quadtree (four-part) prior step k, encoder side

@@ -55,6 +55,19 @@ def ycbcr444_to_420(yuv):
     return np.clip(y, 0., 1.), np.clip(uv, 0., 1.)
 
 
+def png_writer_u8(rgb):
+    """PNGWriter.write_one_frame / HEM save_torch_image (video_writer.py:34-45,
+    DCVC-HEM/test_video.py:68-71): 3 x h x w float32 -> h x w x 3 uint8."""
+    return np.clip(np.rint(rgb.transpose(1, 2, 0) * 255), 0, 255).astype(np.uint8)
+
+
+def yuv_writer_bytes(y, uv):
+    """YUVWriter.write_one_frame with src_format '420' (video_writer.py:100-108)."""
+    y = np.clip(np.rint(y * 255), 0, 255).astype(np.uint8)
+    uv = np.clip(np.rint(uv * 255), 0, 255).astype(np.uint8)
+    return y.tobytes() + uv.tobytes()
+
+
 def calc_psnr(img1, img2, data_range=255):
     """metrics.py:81-92."""
     img1 = img1.astype(np.float64)

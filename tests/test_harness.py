@@ -354,3 +354,82 @@ def test_gpu_rgb_msssim_matches_restatement(h, w):
     got = ms.values(1)[0]
     ref = HO.ms_ssim_torch(torch.from_numpy(rec)[None], torch.from_numpy(src.astype(np.float32) / 255)[None])
     assert abs(got - ref) < 1e-5, (got, ref)
+
+
+# ------------------------------------------------------- decoded-frame writers
+@gpu
+@pytest.mark.parametrize("kind,fmt", [("png", "rgb"), ("yuv", "420"), ("hem_png", "rgb"), ("yuv", "rgb"),
+                                      ("png", "420")])
+def test_recon_writers_match_reference_formulas(tmp_path, kind, fmt):
+    """--save_decoded_frame: what ReconWriter stores for a decoded frame (values
+    outside [0, 1] included, padded buffer cropped) equals the reference's
+    writers applied to the same frame (video_writer.py:26-111 restated in
+    oracle/harness_oracle.py; the 4:2:0 cases through ycbcr444_to_420)."""
+    _need_gpu()
+    from PIL import Image
+    from dcvc_amd import hip as K
+    from dcvc_amd.harness import ReconWriter
+    h, w, H, W = 38, 54, 48, 64
+    g = torch.Generator().manual_seed(3)
+    frames = [torch.rand(H, W, 3, generator=g) * 1.2 - 0.1 for _ in range(2)]
+    wr = ReconWriter(str(tmp_path / "rec"), h, w, kind, fmt, torch.device("cuda", 0))
+    for t, f in enumerate(frames):
+        wr.write(K.Act(f.cuda().contiguous()), t)
+    wr.close()
+    for t, f in enumerate(frames):
+        crop = f[:h, :w].permute(2, 0, 1).numpy()
+        if kind in ("png", "hem_png"):
+            name = f"im{t + 1:05d}.png" if kind == "png" else f"{t}.png"
+            got = np.asarray(Image.open(tmp_path / "rec" / name))
+            if fmt == "rgb":
+                np.testing.assert_array_equal(got, HO.png_writer_u8(crop))
+            else:
+                # 4:2:0 frame into PNGWriter: ycbcr420_to_rgb(order=1) of y_rec, uv_rec
+                y, uv = HO.ycbcr444_to_420(crop)
+                uvz = scipy.ndimage.zoom(uv, (1, 2, 2), order=1)
+                r = y + (2 - 2 * 0.2126) * (uvz[1:2] - 0.5)
+                b = y + (2 - 2 * 0.0722) * (uvz[0:1] - 0.5)
+                gg = (y - 0.2126 * r - 0.0722 * b) / 0.7152
+                np.testing.assert_array_equal(got, HO.png_writer_u8(np.clip(np.concatenate((r, gg, b)), 0, 1)))
+        else:
+            data = (tmp_path / "rec" / "out.yuv").read_bytes()
+            n = h * w * 3 // 2
+            frame = data[t * n:(t + 1) * n]
+            if fmt == "420":
+                y, uv = HO.ycbcr444_to_420(crop)
+            else:
+                kr, kg, kb = 0.2126, 0.7152, 0.0722
+                r, gg, b = crop[0:1], crop[1:2], crop[2:3]
+                y = kr * r + kg * gg + kb * b
+                cb = 0.5 * (b - y) / (1 - kb) + 0.5
+                cr = 0.5 * (r - y) / (1 - kr) + 0.5
+                uv = np.concatenate(HO.ycbcr444_to_420(np.concatenate((y, cb, cr)))[1:], 0)
+                y = np.clip(y, 0, 1)
+            assert frame == HO.yuv_writer_bytes(y, uv)
+
+
+@gpu
+def test_run_test_saves_decoded_frames(dc_golden, tmp_path):
+    """run_test with save_decoded_frame (test_video.py:84-88, 210-221): one
+    PNG per frame, named from 1, in a folder renamed after the averages."""
+    _need_gpu()
+    from dcvc_amd.dc import DMC, IntraNoAR
+    from dcvc_amd.harness import run_test, ArrayReader
+    from dcvc_amd.layers import Precision
+    from dcvc_amd.synth import moving_pattern
+    h, w, n = 100, 130, 3
+    inet = IntraNoAR(precision=Precision.fast()).load_state_dict(dc_golden.i_state_dict())
+    pnet = DMC(precision=Precision.fast()).load_state_dict(dc_golden.p_state_dict())
+    inet.update(force=True)
+    pnet.update(force=True)
+    rec = tmp_path / "dec" / "seq" / "0"
+    log = run_test(pnet, inet, {"frame_num": n, "gop_size": 32, "write_stream": True, "bin_folder": str(tmp_path),
+                                "src_reader": ArrayReader([moving_pattern(h, w, t, seed=3) for t in range(n)]),
+                                "src_type": "png", "src_height": h, "src_width": w, "q_in_ckpt": False,
+                                "i_frame_q_index": 0, "save_decoded_frame": True, "recon_path": str(rec),
+                                "rate_idx": 0, "verbose": 1})
+    folders = [d for d in os.listdir(tmp_path / "dec" / "seq") if d.startswith("0_")]
+    assert len(folders) == 1 and not rec.exists()
+    avg_bpp = sum(b * h * w for b in log["frame_bpp"]) / n / h / w
+    assert folders[0] == f"0_{avg_bpp:.4f}_{log['ave_all_frame_psnr']:.4f}"
+    assert sorted(os.listdir(tmp_path / "dec" / "seq" / folders[0])) == [f"im{i:05d}.png" for i in range(1, n + 1)]
