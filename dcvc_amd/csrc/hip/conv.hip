@@ -84,8 +84,11 @@ __device__ __forceinline__ int swz_off_bf16(int row, int slot) {
   const int x = (0x1320 >> (((row >> 2) & 3) << 2)) & 3;
   return row * 32 + ((slot ^ x) << 3);  // in bf16 elements
 }
-// f32: a row is 32 floats padded to 33.
-__device__ __forceinline__ int off_f32(int row, int k) { return row * 33 + k; }
+// f32: a row is 32 floats padded to 34, so an operand read (ds_read_b32 of 16
+// consecutive rows at k..k+3, 32-lane halves) lands on banks (2 row + hi) % 32:
+// conflict-free (a pad to 33 put rows r and r + 1 of different k on one bank)
+constexpr int kF32Row = 34;
+__device__ __forceinline__ int off_f32(int row, int k) { return row * kF32Row + k; }
 
 template <typename TIN>
 __device__ __forceinline__ float load_in(const ConvP &p, int gy, int gx, int c) {
@@ -293,7 +296,7 @@ __global__ void __launch_bounds__(256) conv_kernel(ConvP p) {
   const int IH = (TH - 1) * S + p.kh;
   const int IW = 15 * S + p.kw;
   const int IWp = (IW + 3) & ~3;
-  const int in_elems = IH * IWp * (F32 ? 33 : 32);
+  const int in_elems = IH * IWp * (F32 ? kF32Row : 32);
   void *lds_in = smem;
   void *lds_w = smem + ((in_elems * (F32 ? 4 : 2) + 15) & ~15);
   float *Lc = reinterpret_cast<float *>(smem + p.lc_off);
@@ -385,7 +388,7 @@ size_t lds_bytes(const ConvP &p, bool wall) {
   const int IH = (TH - 1) * p.s + p.kh;
   const int IW = 15 * p.s + p.kw;
   const int IWp = (IW + 3) & ~3;
-  const size_t row = F32 ? 33 * 4 : 32 * 2;
+  const size_t row = F32 ? kF32Row * 4 : 32 * 2;
   const size_t in_bytes = (size_t)IH * IWp * row;
   const size_t w_bytes = (size_t)(wall ? p.kh : 1) * p.kw * BN * row;
   const size_t stage = ((in_bytes + 15) & ~(size_t)15) + w_bytes;

@@ -11,8 +11,7 @@
 // previous step and written to the other LDS buffer after them (one barrier
 // per step), so the load latency hides behind the matrix work; conv.hip's
 // generic path waited on it twice per 32 channels (47 TF/s at 384->384,
-// 68x120).  LDS rows are 36 floats: the 16 lanes x 4 k of an operand read
-// (rows r..r+15, k..k+3) fall on 64 distinct banks.  Epilogue: epilogue.h.
+// 68x120).  LDS row stride: ldk() below.  Epilogue: epilogue.h.
 #include "common.h"
 #include "epilogue.h"
 
@@ -44,9 +43,12 @@ struct GF {
   int tiles_m;
 };
 
-// LDS row stride: KK + 4 floats, so the 16 lanes x 4 k of an operand read hit
-// 64 distinct banks
-template <int KK> __host__ __device__ constexpr int ldk() { return KK + 4; }
+// LDS row stride: KK + 2 floats.  An operand read is a ds_read_b32 of rows
+// r..r+15 at k..k+3 (lane = 16 hi + col); its 32-lane halves see banks
+// (a / 4) % 32 = (2 col + hi + const) % 32: all distinct, conflict-free (a
+// stride of KK + 4 put col and col + 8 on one bank: 2-way).  Rows are then
+// 8-byte aligned, so staging writes are ds_write_b64.
+template <int KK> __host__ __device__ constexpr int ldk() { return KK + 2; }
 
 template <int BM, int BN, int KK>
 __host__ __device__ constexpr size_t lds_main() {
@@ -129,8 +131,11 @@ __global__ void __launch_bounds__(256) gemm1x1f_kernel(GF p) {
           a = lrelu4(a);
           b = lrelu4(b);
         }
-        *reinterpret_cast<float4 *>(xs + r * kLD + q * 8) = a;
-        *reinterpret_cast<float4 *>(xs + r * kLD + q * 8 + 4) = b;
+        float2 *d = reinterpret_cast<float2 *>(xs + r * kLD + q * 8);
+        d[0] = make_float2(a.x, a.y);
+        d[1] = make_float2(a.z, a.w);
+        d[2] = make_float2(b.x, b.y);
+        d[3] = make_float2(b.z, b.w);
       }
     }
 #pragma unroll
@@ -138,8 +143,11 @@ __global__ void __launch_bounds__(256) gemm1x1f_kernel(GF p) {
       const int it = threadIdx.x + i * 256;
       if (BN * Q % 256 == 0 || it < BN * Q) {
         const int r = it / Q, q = it % Q;
-        *reinterpret_cast<float4 *>(ws + r * kLD + q * 8) = pwa[i];
-        *reinterpret_cast<float4 *>(ws + r * kLD + q * 8 + 4) = pwb[i];
+        float2 *d = reinterpret_cast<float2 *>(ws + r * kLD + q * 8);
+        d[0] = make_float2(pwa[i].x, pwa[i].y);
+        d[1] = make_float2(pwa[i].z, pwa[i].w);
+        d[2] = make_float2(pwb[i].x, pwb[i].y);
+        d[3] = make_float2(pwb[i].z, pwb[i].w);
       }
     }
   };

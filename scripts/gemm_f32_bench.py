@@ -24,18 +24,22 @@ def main():
     ap.add_argument("--cfgs", default="-1,0,1,2,3,4,5,6,7,8,9,10,11")
     ap.add_argument("--H", type=int, default=68)
     ap.add_argument("--W", type=int, default=120)
+    ap.add_argument("--k3", action="store_true", help="time HEM's fp32 3x3 latent convs (conv.hip f32 path) instead")
     a = ap.parse_args()
     import torch
     from dcvc_amd import hip as K
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
     rows = []
-    for cin, cout in SHAPES:
-        cw = K.ConvW(torch.randn(cout, cin, 1, 1) / cin ** 0.5, torch.randn(cout) * 0.1, 1, K.F32, dev)
+    k = 3 if a.k3 else 1
+    shapes = [(384, 288), (480, 384), (192, 192), (288, 288), (128, 128), (64, 64)] if a.k3 else SHAPES
+    cfgs = [-1] if a.k3 else [int(c) for c in a.cfgs.split(",")]
+    for cin, cout in shapes:
+        cw = K.ConvW(torch.randn(cout, cin, k, k) / (cin * k * k) ** 0.5, torch.randn(cout) * 0.1, 1, K.F32, dev)
         x = K.from_nchw(torch.randn(1, cin, a.H, a.W, device=dev), K.F32)
         y = K.conv(cw, x)
         ref = None
-        for cfg in [int(c) for c in a.cfgs.split(",")]:
+        for cfg in cfgs:
             K.set_option("gemm1x1_f32", 0 if cfg < 0 else 1)
             K.set_option("gemm1x1_f32_cfg", max(cfg, 0))
             for _ in range(3):
@@ -50,7 +54,7 @@ def main():
             out = y.t().clone()
             same = True if ref is None else bool(torch.equal(out, ref))
             ref = out if ref is None else ref
-            fl = 2.0 * a.H * a.W * cin * cout
+            fl = 2.0 * a.H * a.W * cin * cout * k * k
             rows.append({"shape": f"{cin}->{cout}", "cfg": cfg, "kernel": K.lib().dcvc_last_kernel().decode(),
                          "us": round(us, 2), "tflops": round(fl / us / 1e6, 1), "bit_identical": same})
             print(json.dumps(rows[-1]), flush=True)
