@@ -522,6 +522,7 @@ extern "C" int dcvc_internal_conv3x3(const dcvc_conv_args *a, void *stream);
 extern "C" void dcvc_internal_conv3x3_resident(int v);
 extern "C" void dcvc_internal_conv3p_enable(int v);
 extern "C" void dcvc_internal_dcbp_enable(int v);
+extern "C" void dcvc_internal_dcbs_enable(int v);
 extern "C" void dcvc_internal_conv3p_occupancy(int v);
 extern "C" void dcvc_internal_gemm1x1_bm(int v);
 
@@ -630,6 +631,10 @@ extern "C" int dcvc_set_option(const char *name, int value) {
   }
   if (std::strcmp(name, "dcb_persistent") == 0) {
     dcvc_internal_dcbp_enable(value);
+    return DCVC_HIP_OK;
+  }
+  if (std::strcmp(name, "dcb_stream") == 0) {
+    dcvc_internal_dcbs_enable(value);
     return DCVC_HIP_OK;
   }
   if (std::strcmp(name, "conv3x3_persistent") == 0) {

@@ -446,6 +446,7 @@ int dispatch(int cin, int cout, bool gated, bool adapt, const DcbP &p, hipStream
 }  // namespace
 
 extern "C" int dcvc_internal_dcbp(const dcvc_dcb_args *a, void *stream);
+extern "C" int dcvc_internal_dcbs(const dcvc_dcb_args *a, void *stream);
 
 extern "C" int dcvc_depthconv_block(const dcvc_dcb_args *a, void *stream) {
   if (!a || !a->x.ptr || !a->y.ptr) return DCVC_HIP_EINVAL;
@@ -458,6 +459,10 @@ extern "C" int dcvc_depthconv_block(const dcvc_dcb_args *a, void *stream) {
   if (!adapt && a->cin != a->cout) return DCVC_HIP_EINVAL;
   {
     const int r = dcvc_internal_dcbp(a, stream);  // persistent resident-weight kernel (dcbp.hip) first
+    if (r != DCVC_HIP_EUNSUPPORTED) return r;
+  }
+  {
+    const int r = dcvc_internal_dcbs(a, stream);  // then persistent streamed-weight kernel (dcbs.hip)
     if (r != DCVC_HIP_EUNSUPPORTED) return r;
   }
   DcbP p{};

@@ -528,13 +528,49 @@ def test_persistent_depthconv_block_equals_per_tile_kernel(shape):
     xa = to_act(torch.randn(1, cin, H, W), h.BF16)
     sc = (torch.rand(cout) + 0.5).cuda()
     outs, names = [], []
-    for pers in (1, 0):
-        h.set_option("dcb_persistent", pers)
-        outs.append(back(blk(xa, scale=sc)))
-        names.append(h.lib().dcvc_last_kernel().decode())
-    h.set_option("dcb_persistent", 1)
+    h.set_option("dcb_stream", 0)
+    try:
+        for pers in (1, 0):
+            h.set_option("dcb_persistent", pers)
+            outs.append(back(blk(xa, scale=sc)))
+            names.append(h.lib().dcvc_last_kernel().decode())
+    finally:
+        h.set_option("dcb_persistent", 1)
+        h.set_option("dcb_stream", 1)
     torch.cuda.synchronize()
     assert names[0].startswith("dcbp_kernel") and names[1].startswith("dcb_kernel"), names
+    assert torch.equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("shape", [(128, 128, False), (128, 64, False), (64, 128, False)])
+@pytest.mark.parametrize("hw", [(133, 541), (21, 35), (272, 480)])
+def test_streamed_depthconv_block_equals_per_tile_kernel(shape, hw):
+    """dcbs.hip (persistent, 8 waves, weights streamed through two LDS
+    buffers two chunks ahead, tiles chained across the stream) vs dcb.hip:
+    same K order and rounding points, so bit-identical; 133x541 gives every
+    workgroup 2-3 tiles, 21x35 fewer tiles than CUs, 272x480 the 1080p
+    quarter-resolution map."""
+    from dcvc_amd import layers as L
+    h = K()
+    cin, cout, gated = shape
+    sd = _dcb_state(cin, cout, gated, seed=cin * 5 + cout)
+    ctx = L.Ctx(sd, torch.device("cuda"), L.Precision.fast())
+    blk = L.DepthConvBlock(ctx, "b", gated=gated)
+    H, W = hw
+    xa = to_act(torch.randn(1, cin, H, W), h.BF16)
+    sc = (torch.rand(cout) + 0.5).cuda()
+    outs, names = [], []
+    h.set_option("dcb_persistent", 0)
+    try:
+        for on in (1, 0):
+            h.set_option("dcb_stream", on)
+            outs.append(back(blk(xa, scale=sc)))
+            names.append(h.lib().dcvc_last_kernel().decode())
+    finally:
+        h.set_option("dcb_stream", 1)
+        h.set_option("dcb_persistent", 1)
+    torch.cuda.synchronize()
+    assert names[0].startswith("dcbs_kernel") and names[1].startswith("dcb_kernel"), names
     assert torch.equal(outs[0], outs[1])
 
 
@@ -595,11 +631,13 @@ def test_copy_and_pad_views(src_dt, dst_dt, coff, C, pad):
     assert not got[:, :, :coff].any() and not got[:, :, coff + C:].any()
 
 
-def test_offset_diversity_paired_bf16_loads_bit_identical():
+@pytest.mark.parametrize("H,W", [(40, 56), (6, 2), (10, 18)])
+def test_offset_diversity_paired_bf16_loads_bit_identical(H, W):
     """bf16 features: the paired-load path (even channel stride / offset) is
-    bit-identical to the per-channel path (odd offset view of a wider buffer)."""
+    bit-identical to the per-channel path (odd offset view of a wider buffer),
+    including a one-column offset map (6x2) and a map whose width is not a
+    multiple of the kernel's pixel tiles (10x18)."""
     h = K()
-    H, W = 40, 56
     feat = torch.randn(1, 48, H, W)
     flow = torch.randn(1, 2, H, W) * 3
     offs = torch.randn(1, 96, H // 2, W // 2) * 0.05
