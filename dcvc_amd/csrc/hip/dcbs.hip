@@ -15,7 +15,7 @@
 //     epilogues) overlaps its SIMD partner's MFMAs;
 //   * weights stream through two 32 KB LDS buffers in 256-row x 64-channel
 //     chunks: conv1 (+ adaptor), conv2, then one chunk per FFN slice (both of
-//     its 1x1 layers) or per two slices; chunk c + 2 is loaded into registers
+//     its 1x1 layers) or per two slices; chunk c + 1 is loaded into registers
 //     while chunk c is in use, the stream runs on across tiles (the weights
 //     do not depend on the tile), one barrier per chunk;
 //   * the adaptor runs in phase 1 and the identity residual is read from
@@ -65,7 +65,12 @@ __device__ __forceinline__ int img(int row, int ch) {
   return row * RL + (((slot ^ ((row >> SH) & MSK)) & (NS - 1)) << 3) + (ch & 7);
 }
 
-__device__ __forceinline__ float lrelu(float v, float s) { return v >= 0.f ? v : v * s; }
+// leaky ReLU as max(v, s * v): the same value as (v >= 0 ? v : s * v) for
+// 0 <= s <= 1 (the host checks), in two VALU instructions instead of three
+__device__ __forceinline__ float lrelu(float v, float s) { return fmaxf(v, v * s); }
+
+__device__ __forceinline__ float4 ld4(const float *p) { return *reinterpret_cast<const float4 *>(p); }
+__device__ __forceinline__ float el(const float4 &v, int q) { return q == 0 ? v.x : q == 1 ? v.y : q == 2 ? v.z : v.w; }
 
 template <int CIN, int COUT, bool ADAPT>
 struct SG {
@@ -91,7 +96,7 @@ struct SG {
   static constexpr int OW = OT + TS + (CS_IN_TS ? 0 : NPI * COUT);
   static_assert(NPI * CIN <= XS && SPC * NPI * 64 <= XS, "Ds / Hs in the input image");
   static constexpr int NA = OW + 2 * WCH;
-  static constexpr size_t LDS = (size_t)NA * 2 + (size_t)10 * CIN * 4;
+  static constexpr size_t LDS = (size_t)NA * 2 + (size_t)10 * CIN * 4 + (size_t)2 * COUT * 4;
   static constexpr int QP = CIN / 8;                         // 16-byte input pieces per pixel
   static constexpr int PP = (NPH * QP + NTHR - 1) / NTHR;    // halo pieces per thread
   // depthwise tasks: (4-channel quad, column, row group) = one thread each
@@ -219,6 +224,7 @@ __global__ void __launch_bounds__(NTHR) dcbs_kernel(DcbP p) {
   uint16_t *const Cs = Xs + G_::OC;
   uint16_t *const Wl = Xs + G_::OW;
   float *const Dw = reinterpret_cast<float *>(Xs + G_::NA);   // [9][CIN] taps, [CIN] bias
+  float *const Lo = Dw + 10 * CIN;                              // [COUT] ffn2 bias, [COUT] scale
 
   const int tid = threadIdx.x;
   const int wave = tid >> 6, lane = tid & 63;
@@ -231,6 +237,7 @@ __global__ void __launch_bounds__(NTHR) dcbs_kernel(DcbP p) {
 
   const __amdgpu_buffer_rsrc_t xr =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t *>(p.x), (short)0, p.xbytes, 0x00020000);
+  int atid = tid;   // thread id for the loaders' addresses (made opaque per tile, see the tile loop)
   // ---- halo input: piece u of thread tid = (halo pixel, 16-byte channel piece)
   u16x8 pf[PP];
   auto issue = [&](int t) {
@@ -238,7 +245,7 @@ __global__ void __launch_bounds__(NTHR) dcbs_kernel(DcbP p) {
     const int base = (oy0 * p.W + ox0) * p.xcs + p.xco;
 #pragma unroll
     for (int u = 0; u < PP; ++u) {
-      const int it = tid + u * NTHR;
+      const int it = atid + u * NTHR;
       const int pix = it / QP, q = it - pix * QP;
       const int hy = pix / HW_, hx = pix - hy * HW_;
       const int gy = oy0 - 1 + hy, gx = ox0 - 1 + hx;
@@ -250,34 +257,34 @@ __global__ void __launch_bounds__(NTHR) dcbs_kernel(DcbP p) {
   auto publish = [&]() {
 #pragma unroll
     for (int u = 0; u < PP; ++u) {
-      const int it = tid + u * NTHR;
+      const int it = atid + u * NTHR;
       const int pix = it / QP, q = it - pix * QP;
       if (it < NPH * QP) *reinterpret_cast<u16x8 *>(Xs + img<CIN>(pix, q * 8)) = pf[u];
     }
   };
 
-  // ---- weight stream: R[c & 1] holds chunk c, loaded two chunks ahead
-  u16x8 R[2][WPT];
-  int atid = tid;   // thread id for the weight stream's addresses (opaque per tile, see below)
-  fetch_head<CIN, COUT, ADAPT, 0>(R[0], p, atid);
-  fetch_chunk<CIN, COUT, ADAPT>(R[1], p, 1, atid);
+  // ---- weight stream: chunk c goes global -> registers while chunk c - 1
+  // is in use, then -> LDS buffer c & 1
+  u16x8 R[WPT];
+  fetch_head<CIN, COUT, ADAPT, 0>(R, p, atid);
   issue(g);
   bool more = g + G < ntiles;
-  // acquire(c, c & 1): chunk c -> LDS buffer c & 1, chunk c + 2 (this tile's
-  // or the next one's) -> registers, one barrier.  Buffer c & 1 was last read
-  // by chunk c - 2's MFMAs, which every wave finished before chunk c - 1's
-  // barrier.  `par` folds to a constant at every call site (R stays in
-  // registers); c may be a run-time value (the FFN loop).
+  // acquire(c, c & 1): chunk c -> LDS buffer c & 1, one barrier, then the
+  // loads of chunk c + 1 (this tile's or the next one's) into R.  Buffer
+  // c & 1 was last read by chunk c - 2's MFMAs, which every wave finished
+  // before chunk c - 1's barrier.  `par` folds to a constant at every call
+  // site; c may be a run-time value (the FFN loop).
   auto acquire = [&](int c, int par) -> const uint16_t * {
     uint16_t *B = Wl + par * WCH;
-    put(B, R[par], atid);
-    const int cn = c + 2 < NCHP ? c + 2 : c + 2 - NCHP;
-    if (c + 2 < NCHP || more) fetch_chunk<CIN, COUT, ADAPT>(R[par], p, cn, atid);
+    put(B, R, atid);
     __syncthreads();
+    const int cn = c + 1 < NCHP ? c + 1 : c + 1 - NCHP;
+    if (c + 1 < NCHP || more) fetch_chunk<CIN, COUT, ADAPT>(R, p, cn, atid);
     return B;
   };
 
   for (int i = tid; i < 10 * CIN; i += NTHR) Dw[i] = i < 9 * CIN ? p.wdw[i] : p.bdw[i - 9 * CIN];
+  for (int i = tid; i < 2 * COUT; i += NTHR) Lo[i] = i < COUT ? p.bf2[i] : (p.scale ? p.scale[i - COUT] : 1.f);
   publish();   // the first tile's halo (chunk 0's barrier publishes it)
 
   constexpr int NQ = G_::NQ, RPT = G_::RPT;
@@ -307,6 +314,9 @@ __global__ void __launch_bounds__(NTHR) dcbs_kernel(DcbP p) {
 
     // ---- P1: t1 = lrelu(conv1(x) + b1) on the halo (0 outside the image);
     // the adaptor on the interior rows of the same image
+    float4 b1v[NTI2];   // loaded before the MFMAs that hide their latency
+#pragma unroll
+    for (int j = 0; j < NTI2; ++j) b1v[j] = ld4(p.b1 + (hf * NTI2 + j) * 16 + hi * 4);
     const uint16_t *B0 = acquire(0, 0);
     f32x4 ad[2][ADAPT ? NTO2 : 1];
     {
@@ -333,7 +343,7 @@ __global__ void __launch_bounds__(NTHR) dcbs_kernel(DcbP p) {
             const int c = (hf * NTI2 + j) * 16 + hi * 4;
             float v[4];
 #pragma unroll
-            for (int q = 0; q < 4; ++q) v[q] = inside ? lrelu(acc[i][j][q] + p.b1[c + q], p.slope_dc) : 0.f;
+            for (int q = 0; q < 4; ++q) v[q] = inside ? lrelu(acc[i][j][q] + el(b1v[j], q), p.slope_dc) : 0.f;
             put4<CIN>(Ts, row, c, v);
           }
         }
@@ -353,6 +363,12 @@ __global__ void __launch_bounds__(NTHR) dcbs_kernel(DcbP p) {
           res[i][j] = __builtin_bit_cast(u16x4, __builtin_amdgcn_raw_buffer_load_b64(xr, off, 0, 0));
         }
       }
+    }
+    float4 b2v[NTO2], bav[ADAPT ? NTO2 : 1];
+#pragma unroll
+    for (int j = 0; j < NTO2; ++j) {
+      b2v[j] = ld4(p.b2 + (hf * NTO2 + j) * 16 + hi * 4);
+      if constexpr (ADAPT) bav[j] = ld4(p.ba + (hf * NTO2 + j) * 16 + hi * 4);
     }
     // conv2's chunk; its barrier also publishes t1 (and ends every read of x)
     const uint16_t *B2 = acquire(G_::C_CONV2, G_::C_CONV2 & 1);
@@ -414,9 +430,9 @@ __global__ void __launch_bounds__(NTHR) dcbs_kernel(DcbP p) {
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
             if constexpr (ADAPT)
-              v[q] = bf2f(f2bf(ad[i][j][q] + p.ba[c + q])) + (dc[i][j][q] + p.b2[c + q]);
+              v[q] = bf2f(f2bf(ad[i][j][q] + el(bav[j], q))) + (dc[i][j][q] + el(b2v[j], q));
             else
-              v[q] = (dc[i][j][q] + p.b2[c + q]) + bf2f(res[i][j][q]);
+              v[q] = (dc[i][j][q] + el(b2v[j], q)) + bf2f(res[i][j][q]);
           }
           put4<COUT>(Cs, rowi[i] + col, c, v);   // Ts (t1) was last read before P2's barrier
         }
@@ -441,6 +457,9 @@ __global__ void __launch_bounds__(NTHR) dcbs_kernel(DcbP p) {
           const int s = f * SPC + ss;
           const uint16_t *Bs = B + ss * RS * 64;
           uint16_t *Hs = Xs + ss * NPI * 64;
+          float4 f1v[2];
+#pragma unroll
+          for (int j = 0; j < 2; ++j) f1v[j] = ld4(p.bf1 + s * 64 + (hf * 2 + j) * 16 + hi * 4);
           f32x4 hacc[2][2];
           zero(hacc);
 #pragma unroll
@@ -452,7 +471,7 @@ __global__ void __launch_bounds__(NTHR) dcbs_kernel(DcbP p) {
               const int c = (hf * 2 + j) * 16 + hi * 4;
               float v[4];
 #pragma unroll
-              for (int q = 0; q < 4; ++q) v[q] = lrelu(hacc[i][j][q] + p.bf1[s * 64 + c + q], p.slope_ffn);
+              for (int q = 0; q < 4; ++q) v[q] = lrelu(hacc[i][j][q] + el(f1v[j], q), p.slope_ffn);
               put4<64>(Hs, rowi[i] + col, c, v);
             }
           __syncthreads();   // hidden slice published
@@ -469,11 +488,12 @@ __global__ void __launch_bounds__(NTHR) dcbs_kernel(DcbP p) {
         const int c = (hf * NTO2 + j) * 16 + hi * 4;
         u16x4 *cp = reinterpret_cast<u16x4 *>(Cs + img<COUT>(rowi[i] + col, c));
         const u16x4 dcv = *cp;
+        const float4 f2v = ld4(Lo + c), scv = ld4(Lo + COUT + c);
         u16x4 o;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          float v = bf2f(dcv[q]) + lrelu(acc[i][j][q] + p.bf2[c + q], p.slope_ffn);
-          if (p.scale) v = v * p.scale[c + q];
+          float v = bf2f(dcv[q]) + lrelu(acc[i][j][q] + el(f2v, q), p.slope_ffn);
+          if (p.scale) v = v * el(scv, q);
           o[q] = f2bf(v);
         }
         *cp = o;
@@ -528,6 +548,8 @@ int run(DcbP p, hipStream_t st) {
 // dcbp.hip declined; DCVC_HIP_EUNSUPPORTED hands the call to dcb_kernel.
 extern "C" int dcvc_internal_dcbs(const dcvc_dcb_args *a, void *stream) {
   if (!g_enabled || a->gated) return DCVC_HIP_EUNSUPPORTED;
+  if (!(a->slope_dc >= 0.f && a->slope_dc <= 1.f && a->slope_ffn >= 0.f && a->slope_ffn <= 1.f))
+    return DCVC_HIP_EUNSUPPORTED;   // lrelu as max(v, s v)
   if ((int64_t)a->x.H * a->x.W * a->x.cstride >= ((int64_t)1 << 30) - 16) return DCVC_HIP_EUNSUPPORTED;
   const bool adapt = a->w_adaptor != nullptr;
   // the streamed chunks are whole 64-channel pieces of the packed weights
