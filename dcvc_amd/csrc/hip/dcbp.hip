@@ -60,7 +60,9 @@ __device__ __forceinline__ int img(int row, int ch) {
 template <int C>
 constexpr int rl() { return C <= 32 ? 32 : (C <= 64 ? 64 : 128); }
 
-__device__ __forceinline__ float lrelu(float v, float s) { return v >= 0.f ? v : v * s; }
+// leaky ReLU as max(v, s * v): the same value as (v >= 0 ? v : s * v) for
+// 0 <= s <= 1 (the host checks), in two VALU instructions instead of three
+__device__ __forceinline__ float lrelu(float v, float s) { return fmaxf(v, v * s); }
 
 template <int CIN, int COUT, bool ADAPT>
 struct DG {
@@ -86,6 +88,7 @@ struct DG {
   static constexpr size_t LDS = (size_t)NW * 2 + (size_t)NA * 2 + (size_t)NC * 4;
   static constexpr int QP = CIN / 8;
   static constexpr int PP = (NPH * QP + NTHR - 1) / NTHR;   // prefetch pieces per thread
+  static_assert((NW + NA) % 8 == 0 && CDW % 4 == 0 && CIN % 4 == 0, "16-byte aligned depthwise taps");
 };
 
 // acc[i][j] += A[16j + ..][k] * B[row_i + col][k], k in [0, K)
@@ -258,28 +261,57 @@ __global__ void __launch_bounds__(NTHR) dcbp_kernel(DcbP p) {
     }
     __syncthreads();
 
-    // ---- P2: d = dw3x3(t1) + bdw on interior pixels
-    for (int it = tid; it < NPI * (RLI / 8); it += NTHR) {
-      const int pix = it / (RLI / 8), s = it % (RLI / 8);
-      const int r = pix / TW, c = pix % TW;
-      u16x8 o{};
-      if (s * 8 < CIN) {
-        float acc[8];
+    // ---- P2: d = dw3x3(t1) + bdw on interior pixels: each thread a column
+    // of RPT output pixels x 4 channels, every t1 value converted once
+    {
+      constexpr int NQ = RLI / 4, NRG = NTHR / (NQ * TW), RPT = TH / NRG;
+      static_assert(NQ * TW * NRG == NTHR && RPT * NRG == TH, "depthwise tasks");
+      const int dq = tid % NQ, dcol = (tid / NQ) % TW, drg = tid / (NQ * TW);
+      if (dq * 4 < CIN) {
+        float w[9][4], bias[4];
 #pragma unroll
-        for (int q = 0; q < 8; ++q) acc[q] = 0.f;
-#pragma unroll
-        for (int dy = 0; dy < 3; ++dy)
+        for (int k = 0; k < 9; ++k) {
+          const float4 v = *reinterpret_cast<const float4 *>(Dw + k * CIN + dq * 4);
+          w[k][0] = v.x; w[k][1] = v.y; w[k][2] = v.z; w[k][3] = v.w;
+        }
+        {
+          const float4 v = *reinterpret_cast<const float4 *>(Dw + 9 * CIN + dq * 4);
+          bias[0] = v.x; bias[1] = v.y; bias[2] = v.z; bias[3] = v.w;
+        }
+        float tv[3][3][4];   // rolling window: t1 row r in tv[r % 3]
+        auto load_row = [&](int r) {
 #pragma unroll
           for (int dx = 0; dx < 3; ++dx) {
-            const u16x8 tv = *reinterpret_cast<const u16x8 *>(Ts + img<RLI>((r + dy) * HW_ + c + dx, s * 8));
-            const float *w = Dw + (dy * 3 + dx) * CIN + s * 8;
+            const u16x4 v = *reinterpret_cast<const u16x4 *>(Ts + img<RLI>((drg * RPT + r) * HW_ + dcol + dx, dq * 4));
 #pragma unroll
-            for (int q = 0; q < 8; ++q) acc[q] += w[q] * bf2f(tv[q]);
+            for (int q = 0; q < 4; ++q) tv[r % 3][dx][q] = bf2f(v[q]);
           }
+        };
+        load_row(0);
+        load_row(1);
 #pragma unroll
-        for (int q = 0; q < 8; ++q) o[q] = f2bf(acc[q] + Dw[9 * CIN + s * 8 + q]);
+        for (int o = 0; o < RPT; ++o) {
+          load_row(o + 2);
+          float acc[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+            for (int dx = 0; dx < 3; ++dx)
+#pragma unroll
+              for (int q = 0; q < 4; ++q) acc[q] = __builtin_fmaf(w[dy * 3 + dx][q], tv[(o + dy) % 3][dx][q], acc[q]);
+          float v[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) v[q] = acc[q] + bias[q];
+          u16x4 o4;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) o4[q] = f2bf(v[q]);
+          *reinterpret_cast<u16x4 *>(Ds + img<RLI>((drg * RPT + o) * TW + dcol, dq * 4)) = o4;
+        }
+      } else {
+#pragma unroll
+        for (int o = 0; o < RPT; ++o)
+          *reinterpret_cast<u16x4 *>(Ds + img<RLI>((drg * RPT + o) * TW + dcol, dq * 4)) = u16x4{0, 0, 0, 0};
       }
-      *reinterpret_cast<u16x8 *>(Ds + img<RLI>(pix, s * 8)) = o;
     }
     __syncthreads();
 
@@ -332,7 +364,9 @@ __global__ void __launch_bounds__(NTHR) dcbp_kernel(DcbP p) {
         put4<RLO>(Cs, pix, c, v);
       }
     }
-    __syncthreads();  // Cs published; Ds (d) fully read before Hs overwrites it
+    // From here to P5 every wave touches only its own pixel tile's rows of
+    // Cs, Ds / Hs and (read-only) Xs: a wave's LDS operations complete in
+    // order, so P3 -> P4 -> P5 need no barriers.
 
     // ---- P4: FFN over 64-channel hidden slices
     f32x4 acc[NPT][NTO];
@@ -348,7 +382,6 @@ __global__ void __launch_bounds__(NTHR) dcbp_kernel(DcbP p) {
 #pragma unroll
         for (int j = 0; j < NTH; ++j) hacc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
       mma<RLO, RLO, NPT, NTH>(hacc, Cs, rowi, Wl + G_::OF1 + s * 64 * RLO, COUT, lane);
-      if (s > 0) __syncthreads();  // previous slice's Hs fully read
 #pragma unroll
       for (int i = 0; i < NPT; ++i)
 #pragma unroll
@@ -358,10 +391,8 @@ __global__ void __launch_bounds__(NTHR) dcbp_kernel(DcbP p) {
           for (int q = 0; q < 4; ++q) v[q] = lrelu(hacc[i][j][q] + bf1[s * 64 + j * 16 + hi * 4 + q], p.slope_ffn);
           put4<64>(Hs, rowi[i] + col, j * 16 + hi * 4, v);
         }
-      __syncthreads();
       mma<64, 64, NPT, NTO>(acc, Hs, rowi, Wl + G_::OF2 + s * NTO * 16 * 64, 64, lane);
     }
-    __syncthreads();  // every wave done with Cs (FFN input) and Hs
 
     // ---- P5: out = dc + lrelu(acc + bf2) [* scale] -> Cs (bf16), whole-line stores
 #pragma unroll
@@ -382,7 +413,7 @@ __global__ void __launch_bounds__(NTHR) dcbp_kernel(DcbP p) {
         *reinterpret_cast<u16x4 *>(Cs + img<RLO>(pix, c)) = o;
       }
     }
-    __syncthreads();
+    __syncthreads();   // every wave's output rows in Cs
     constexpr int NSO = COUT / 8;
     for (int it = tid; it < NPI * NSO; it += NTHR) {
       const int pix = it / NSO, s8 = (it % NSO) * 8;
@@ -433,6 +464,8 @@ int run(DcbP p, hipStream_t st) {
 // non-gated blocks; DCVC_HIP_EUNSUPPORTED hands the call to dcb_kernel.
 extern "C" int dcvc_internal_dcbp(const dcvc_dcb_args *a, void *stream) {
   if (!g_enabled || a->gated) return DCVC_HIP_EUNSUPPORTED;
+  if (!(a->slope_dc >= 0.f && a->slope_dc <= 1.f && a->slope_ffn >= 0.f && a->slope_ffn <= 1.f))
+    return DCVC_HIP_EUNSUPPORTED;   // lrelu as max(v, s v)
   if ((int64_t)a->x.H * a->x.W * a->x.cstride >= ((int64_t)1 << 30) - 16) return DCVC_HIP_EUNSUPPORTED;
   const bool adapt = a->w_adaptor != nullptr;
   DcbP p{};

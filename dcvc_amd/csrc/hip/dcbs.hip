@@ -9,10 +9,12 @@
 // ascending in 32-wide steps), so outputs are bit-identical to it
 // (tests/test_gpu_kernels.py).  The organisation is built for one workgroup
 // per CU (the activations take ~100 KB of LDS) running at two waves per SIMD:
-//   * 8 waves; wave w works on pixel tiles {w % 4, w % 4 + 4, ...} and on the
-//     output-channel half w / 4 of every GEMM, so operand reuse per LDS read
-//     stays at 0.6-1 reads per MFMA, and one wave's VALU work (depthwise,
-//     epilogues) overlaps its SIMD partner's MFMAs;
+//   * 8 waves; in conv1 / adaptor / conv2 wave w works on pixel tiles
+//     {w % 4, w % 4 + 4, ...} and output-channel half w / 4 (0.6-0.75 LDS
+//     reads per MFMA); in the FFN on pixel tile w and all channels, so its
+//     hidden slices stay wave-private (no barrier between the two FFN
+//     GEMMs); one wave's VALU work (depthwise, epilogues) overlaps its SIMD
+//     partner's MFMAs;
 //   * weights stream through two 32 KB LDS buffers in 256-row x 64-channel
 //     chunks: conv1 (+ adaptor), conv2, then one chunk per FFN slice (both of
 //     its 1x1 layers) or per two slices; chunk c + 1 is loaded into registers
@@ -94,7 +96,7 @@ struct SG {
   static constexpr bool CS_IN_TS = NPI * COUT <= TS;
   static constexpr int OT = XS, OC = CS_IN_TS ? OT : OT + TS;
   static constexpr int OW = OT + TS + (CS_IN_TS ? 0 : NPI * COUT);
-  static_assert(NPI * CIN <= XS && SPC * NPI * 64 <= XS, "Ds / Hs in the input image");
+  static_assert(NPI * CIN <= XS && NPI * 64 <= XS, "Ds / Hs in the input image");
   static constexpr int NA = OW + 2 * WCH;
   static constexpr size_t LDS = (size_t)NA * 2 + (size_t)10 * CIN * 4 + (size_t)2 * COUT * 4;
   static constexpr int QP = CIN / 8;                         // 16-byte input pieces per pixel
@@ -440,64 +442,62 @@ __global__ void __launch_bounds__(NTHR) dcbs_kernel(DcbP p) {
     // the next tile's halo: in flight during the FFN, written to Xs in P5
     if (more) issue(tn);
 
-    // ---- P4: FFN, one or two 64-channel hidden slices per weight chunk
-    f32x4 acc[2][NTO2];
+    // ---- P4: FFN, one or two 64-channel hidden slices per weight chunk.
+    // Wave w owns pixel tile w here (all channels): its hidden slice rows in
+    // Hs are written and read by itself only, and a wave's LDS operations
+    // complete in order, so no barrier separates ffn1 from ffn2.
+    constexpr int NTO = COUT / 16;
+    const int rowf[1] = {wave * 16};
+    f32x4 acc[1][NTO];
     zero(acc);
+    uint16_t *const Hs = Xs;
 #pragma unroll 1
     for (int fp = 0; fp < G_::NFC; fp += 2)
 #pragma unroll
       for (int fu = 0; fu < 2; ++fu) {
         if ((G_::NFC & 1) && fp + fu >= G_::NFC) break;
         const int f = fp + fu;
-        // publishes chunk f (and, the first time, Cs); every wave is past
-        // the previous chunk's hidden-slice reads
+        // publishes chunk f (and, the first time, Cs)
         const uint16_t *B = acquire(G_::C_FFN + f, (G_::C_FFN + fu) & 1);
 #pragma unroll
         for (int ss = 0; ss < SPC; ++ss) {
           const int s = f * SPC + ss;
           const uint16_t *Bs = B + ss * RS * 64;
-          uint16_t *Hs = Xs + ss * NPI * 64;
-          float4 f1v[2];
+          float4 f1v[4];
 #pragma unroll
-          for (int j = 0; j < 2; ++j) f1v[j] = ld4(p.bf1 + s * 64 + (hf * 2 + j) * 16 + hi * 4);
-          f32x4 hacc[2][2];
+          for (int j = 0; j < 4; ++j) f1v[j] = ld4(p.bf1 + s * 64 + j * 16 + hi * 4);
+          f32x4 hacc[1][4];
           zero(hacc);
 #pragma unroll
-          for (int kc = 0; kc < KCO; ++kc) mma<COUT, 2, 2>(hacc, Cs, rowi, Bs + kc * 64 * 64, hf * 2, lane_, kc * 64);
+          for (int kc = 0; kc < KCO; ++kc) mma<COUT, 1, 4>(hacc, Cs, rowf, Bs + kc * 64 * 64, 0, lane_, kc * 64);
 #pragma unroll
-          for (int i = 0; i < 2; ++i)
+          for (int j = 0; j < 4; ++j) {
+            float v[4];
 #pragma unroll
-            for (int j = 0; j < 2; ++j) {
-              const int c = (hf * 2 + j) * 16 + hi * 4;
-              float v[4];
-#pragma unroll
-              for (int q = 0; q < 4; ++q) v[q] = lrelu(hacc[i][j][q] + el(f1v[j], q), p.slope_ffn);
-              put4<64>(Hs, rowi[i] + col, c, v);
-            }
-          __syncthreads();   // hidden slice published
-          mma<64, 2, NTO2>(acc, Hs, rowi, Bs + KCO * 64 * 64, hf * NTO2, lane_, 0);
+            for (int q = 0; q < 4; ++q) v[q] = lrelu(hacc[0][j][q] + el(f1v[j], q), p.slope_ffn);
+            put4<64>(Hs, rowf[0] + col, j * 16 + hi * 4, v);
+          }
+          mma<64, 1, NTO>(acc, Hs, rowf, Bs + KCO * 64 * 64, 0, lane_, 0);
         }
       }
 
-    // ---- P5: out = dc + lrelu(acc + bf2) [* scale] -> Cs (each lane over
-    // its own P3 values), whole-line stores
+    // ---- P5: out = dc + lrelu(acc + bf2) [* scale] -> Cs (each wave over
+    // its own pixel tile's rows), whole-line stores
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int j = 0; j < NTO; ++j) {
+      const int c = j * 16 + hi * 4;
+      u16x4 *cp = reinterpret_cast<u16x4 *>(Cs + img<COUT>(rowf[0] + col, c));
+      const u16x4 dcv = *cp;
+      const float4 f2v = ld4(Lo + c), scv = ld4(Lo + COUT + c);
+      u16x4 o;
 #pragma unroll
-      for (int j = 0; j < NTO2; ++j) {
-        const int c = (hf * NTO2 + j) * 16 + hi * 4;
-        u16x4 *cp = reinterpret_cast<u16x4 *>(Cs + img<COUT>(rowi[i] + col, c));
-        const u16x4 dcv = *cp;
-        const float4 f2v = ld4(Lo + c), scv = ld4(Lo + COUT + c);
-        u16x4 o;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          float v = bf2f(dcv[q]) + lrelu(acc[i][j][q] + el(f2v, q), p.slope_ffn);
-          if (p.scale) v = v * el(scv, q);
-          o[q] = f2bf(v);
-        }
-        *cp = o;
+      for (int q = 0; q < 4; ++q) {
+        float v = bf2f(dcv[q]) + lrelu(acc[0][j][q] + el(f2v, q), p.slope_ffn);
+        if (p.scale) v = v * el(scv, q);
+        o[q] = f2bf(v);
       }
+      *cp = o;
+    }
     if constexpr (NCHP != NCH) acquire(NCH, NCH & 1);   // padding chunk: keeps the parity, gives the barrier
     else __syncthreads();
     if (more) publish();   // Xs (Ds / Hs) is dead: the last hidden slice was read before this barrier
