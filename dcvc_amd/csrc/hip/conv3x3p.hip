@@ -164,8 +164,7 @@ __global__ void __launch_bounds__(NW * 64) conv3p_kernel(P3 p) {
   // it on the spot, which would serialise the prefetch)
   const __amdgpu_buffer_rsrc_t xr =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t *>(p.x), (short)0, p.xbytes, 0x00020000);
-  u16x8 pf[PP];
-  auto issue = [&](int t) {
+  auto issue = [&](int t, u16x8 (&pf)[PP]) {
     const int oy0 = (t / p.tiles_x) * TH, ox0 = (t % p.tiles_x) * 16;
     const int base = (oy0 * p.W + ox0) * p.xcs;
 #pragma unroll
@@ -177,7 +176,7 @@ __global__ void __launch_bounds__(NW * 64) conv3p_kernel(P3 p) {
       pf[u] = __builtin_bit_cast(u16x8, v);
     }
   };
-  auto publish = [&]() {
+  auto publish = [&](const u16x8 (&pf)[PP]) {
     if (p.in_lrelu) {
 #pragma unroll
       for (int u = 0; u < PP; ++u) {
@@ -197,7 +196,14 @@ __global__ void __launch_bounds__(NW * 64) conv3p_kernel(P3 p) {
     }
   };
 
-  issue(g);
+  // input tiles two ahead: tile t's halo is loaded while tiles t - 2G and
+  // t - G run (two register sets, alternating between consecutive tiles)
+  // (16-row tiles only: for 8-row tiles, 128->64 at 1/2 resolution, one
+  // tile ahead measured faster)
+  constexpr bool kDeep = RW == 2;
+  u16x8 pfa[PP], pfb[PP];
+  issue(g, pfa);
+  if (kDeep && g + G < ntiles) issue(g + G, pfb);
   // ---- resident weights [KS][BN][32] (swizzled by row) + epilogue constants
   for (int it = tid; it < KS * BN * 4; it += NTHR) {
     const int row = it >> 2, sl = it & 3;
@@ -241,49 +247,62 @@ __global__ void __launch_bounds__(NW * 64) conv3p_kernel(P3 p) {
   const __amdgpu_buffer_rsrc_t rr2 =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p.res2), (short)0, p.r2bytes, 0x00020000);
 
-  for (int t = g;;) {
-    publish();
+  // epilogue-B piece u of tile t: 8 consecutive output channels of one
+  // output pixel, in output-row order (SHUF: conv channel n of pixel (y, x)
+  // is output channel n >> 2 of pixel (2y + (n >> 1 & 1), 2x + (n & 1)),
+  // pixel_shuffle(2)); ob = output pixel index, src = its fp32 tile offset
+  auto piece = [&](int t, int u, int64_t &ob, int &src, int &cq, bool &ok) {
+    const int oy0 = (t / p.tiles_x) * TH, ox0 = (t % p.tiles_x) * 16;
+    constexpr int NQ = SHUF ? BN / 32 : BN / 8;  // pieces per (pixel, sub-position)
+    const int it = tid + u * NTHR;
+    const int q = it % NQ, r = it / NQ;
+    int l, oy, ox;
+    if constexpr (SHUF) {
+      const int dx = r & 1, cx = (r >> 1) & 15, dy = (r >> 5) & 1, cyl = r >> 6;
+      l = cyl * 16 + cx;
+      oy = 2 * (oy0 + cyl) + dy;
+      ox = 2 * (ox0 + cx) + dx;
+      ok = it < TH * 16 * 4 * NQ && oy0 + cyl < p.H && ox0 + cx < p.W;
+      src = l * LD + 4 * q * 8 + dy * 2 + dx;
+    } else {
+      l = r;
+      oy = oy0 + (l >> 4);
+      ox = ox0 + (l & 15);
+      ok = it < TH * 16 * NQ && oy < p.H && ox < p.W;
+      src = l * LD + q * 8;
+    }
+    cq = q * 8;
+    ob = (int64_t)oy * p.Wout + ox;
+  };
+  // residual pieces of tile t, loaded right after tile t - G's epilogue has
+  // consumed its own, so their HBM latency hides behind tile t's publish and
+  // MFMAs
+  typedef typename Vec8<TOUT>::raw RV;
+  auto load_res = [&](int t, RV (&r1)[PO], RV (&r2)[PO]) {
+#pragma unroll
+    for (int u = 0; u < PO; ++u) {
+      int64_t ob;
+      int src, cq;
+      bool ok;
+      piece(t, u, ob, src, cq, ok);
+      const int cb = (SHUF ? n0 / 4 : n0) + cq;
+      if (p.res) r1[u] = Vec8<TOUT>::load(rr, ok ? (int)(ob * p.rcs + p.rco + cb) : -1);
+      if (p.res2) r2[u] = Vec8<TOUT>::load(rr2, ok ? (int)(ob * p.r2cs + p.r2co + cb) : -1);
+    }
+  };
+  RV ra1[PO], ra2[PO];
+  load_res(g, ra1, ra2);
+
+  // one tile; returns whether this workgroup has a next one
+  auto tile = [&](int t, u16x8 (&pf)[PP], RV (&r1)[PO], RV (&r2)[PO]) -> bool {
+    publish(pf);
     __syncthreads();
     const int tn = t + G;
     const bool more = tn < ntiles;
-    if (more) issue(tn);  // in flight across this tile's MFMAs and epilogue
-    // epilogue-B plan and residual loads for this tile, issued before the
-    // MFMAs so their HBM latency hides behind them (pieces of 8 consecutive
-    // output channels of one output pixel, in output-row order; SHUF: conv
-    // channel n of pixel (y, x) is output channel n >> 2 of pixel
-    // (2y + (n >> 1 & 1), 2x + (n & 1)), pixel_shuffle(2))
-    int64_t ob[PO];
-    int src[PO], cq[PO];
-    bool ok[PO];
-    typename Vec8<TOUT>::raw r1[PO], r2[PO];
-    {
-      const int oy0 = (t / p.tiles_x) * TH, ox0 = (t % p.tiles_x) * 16;
-      constexpr int NQ = SHUF ? BN / 32 : BN / 8;  // pieces per (pixel, sub-position)
-#pragma unroll
-      for (int u = 0; u < PO; ++u) {
-        const int it = tid + u * NTHR;
-        const int q = it % NQ, r = it / NQ;
-        int l, oy, ox;
-        if constexpr (SHUF) {
-          const int dx = r & 1, cx = (r >> 1) & 15, dy = (r >> 5) & 1, cyl = r >> 6;
-          l = cyl * 16 + cx;
-          oy = 2 * (oy0 + cyl) + dy;
-          ox = 2 * (ox0 + cx) + dx;
-          ok[u] = it < TH * 16 * 4 * NQ && oy0 + cyl < p.H && ox0 + cx < p.W;
-          src[u] = l * LD + 4 * q * 8 + dy * 2 + dx;
-        } else {
-          l = r;
-          oy = oy0 + (l >> 4);
-          ox = ox0 + (l & 15);
-          ok[u] = it < TH * 16 * NQ && oy < p.H && ox < p.W;
-          src[u] = l * LD + q * 8;
-        }
-        cq[u] = q * 8;
-        ob[u] = (int64_t)oy * p.Wout + ox;
-        const int cb = (SHUF ? n0 / 4 : n0) + q * 8;
-        if (p.res) r1[u] = Vec8<TOUT>::load(rr, ok[u] ? (int)(ob[u] * p.rcs + p.rco + cb) : -1);
-        if (p.res2) r2[u] = Vec8<TOUT>::load(rr2, ok[u] ? (int)(ob[u] * p.r2cs + p.r2co + cb) : -1);
-      }
+    if (kDeep) {
+      if (tn + G < ntiles) issue(tn + G, pf);  // in flight across the next two tiles
+    } else if (more) {
+      issue(tn, pf);
     }
 
     f32x4 acc[RW][NT];
@@ -355,14 +374,18 @@ __global__ void __launch_bounds__(NW * 64) conv3p_kernel(P3 p) {
     {
 #pragma unroll
       for (int u = 0; u < PO; ++u) {
-        if (!ok[u]) continue;
+        int64_t ob;
+        int src, cq;
+        bool ok;
+        piece(t, u, ob, src, cq, ok);
+        if (!ok) continue;
         float v[8];
         if constexpr (SHUF) {
 #pragma unroll
-          for (int j = 0; j < 8; ++j) v[j] = T[src[u] + 4 * j];
+          for (int j = 0; j < 8; ++j) v[j] = T[src + 4 * j];
         } else {
-          const float4 a = *reinterpret_cast<const float4 *>(T + src[u]);
-          const float4 b = *reinterpret_cast<const float4 *>(T + src[u] + 4);
+          const float4 a = *reinterpret_cast<const float4 *>(T + src);
+          const float4 b = *reinterpret_cast<const float4 *>(T + src + 4);
           v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
           v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
         }
@@ -376,14 +399,21 @@ __global__ void __launch_bounds__(NW * 64) conv3p_kernel(P3 p) {
         }
         if (p.scale) {
 #pragma unroll
-          for (int j = 0; j < 8; ++j) v[j] = v[j] * Lc[BN + cq[u] + j];
+          for (int j = 0; j < 8; ++j) v[j] = v[j] * Lc[BN + cq + j];
         }
-        Vec8<TOUT>::store(reinterpret_cast<TOUT *>(p.y) + ob[u] * p.ycs + p.yco + (SHUF ? n0 / 4 : n0) + cq[u], v);
+        Vec8<TOUT>::store(reinterpret_cast<TOUT *>(p.y) + ob * p.ycs + p.yco + (SHUF ? n0 / 4 : n0) + cq, v);
       }
     }
-    if (!more) break;
+    if (!more) return false;
+    load_res(tn, r1, r2);   // the next tile's residual pieces, in flight during its publish and MFMAs
     __syncthreads();  // T read by every thread before the next image overwrites it
-    t = tn;
+    return true;
+  };
+  for (int t = g;;) {
+    if (!tile(t, pfa, ra1, ra2)) break;
+    t += G;
+    if (!tile(t, kDeep ? pfb : pfa, ra1, ra2)) break;
+    t += G;
   }
 }
 

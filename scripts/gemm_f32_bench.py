@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--H", type=int, default=68)
     ap.add_argument("--W", type=int, default=120)
     ap.add_argument("--k3", action="store_true", help="time HEM's fp32 3x3 latent convs (conv.hip f32 path) instead")
+    ap.add_argument("--shapes", default="", help="cin x cout list, e.g. 384x384,1024x384")
     a = ap.parse_args()
     import torch
     from dcvc_amd import hip as K
@@ -33,6 +34,8 @@ def main():
     rows = []
     k = 3 if a.k3 else 1
     shapes = [(384, 288), (480, 384), (192, 192), (288, 288), (128, 128), (64, 64)] if a.k3 else SHAPES
+    if a.shapes:
+        shapes = [tuple(int(v) for v in sh.split("x")) for sh in a.shapes.split(",")]
     cfgs = [-1] if a.k3 else [int(c) for c in a.cfgs.split(",")]
     for cin, cout in shapes:
         cw = K.ConvW(torch.randn(cout, cin, k, k) / (cin * k * k) ** 0.5, torch.randn(cout) * 0.1, 1, K.F32, dev)
