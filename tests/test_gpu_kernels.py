@@ -574,6 +574,45 @@ def test_streamed_depthconv_block_equals_per_tile_kernel(shape, hw):
     assert torch.equal(outs[0], outs[1])
 
 
+@pytest.mark.parametrize("cin,cout,H,W,res,out32", [(8, 32, 544, 960, False, False), (16, 2, 544, 960, True, True),
+                                                    (8, 32, 37, 45, False, False), (16, 2, 21, 19, True, True),
+                                                    (8, 16, 40, 70, True, False)])
+def test_conv7_small_cin_matches_torch(cin, cout, H, W, res, out32):
+    """conv7s.hip (SpyNet's 8- and 16-channel 7x7 layers, taps packed into
+    the MFMA K dimension) vs torch fp32 on the bf16-rounded operands and vs
+    the generic conv.hip path; 544x960 gives each persistent workgroup
+    several tiles, the small maps partial tiles."""
+    h = K()
+    x = torch.randn(1, cin, H, W)
+    w = torch.randn(cout, cin, 7, 7) / (cin * 49) ** 0.5
+    b = torch.randn(cout) * 0.1
+    r = torch.randn(1, cout, H, W) if res else None
+    xb = x.bfloat16().float()
+    ref = F.conv2d(xb, w.bfloat16().float(), b, padding=3)
+    if not res:
+        ref = F.relu(ref)
+    else:
+        ref = ref + r
+    cw = h.ConvW(w, b, 1, h.BF16)
+    xa = to_act(x, h.BF16)
+    odt = h.F32 if out32 else h.BF16
+    ra = to_act(r, odt) if res else None
+    outs, names = [], []
+    for on in (1, 0):
+        h.set_option("conv7_small_cin", on)
+        try:
+            y = h.conv(cw, xa, out_dtype=odt, act=h.ACT_NONE if res else h.ACT_LRELU, slope=0.0, res=ra)
+        finally:
+            h.set_option("conv7_small_cin", 1)
+        outs.append(back(y))
+        names.append(h.lib().dcvc_last_kernel().decode())
+    torch.cuda.synchronize()
+    assert names[0].startswith("conv7s_kernel") and names[1].startswith("conv_kernel"), names
+    tol = 2e-5 if out32 else 1e-2   # fp32 sums of exact bf16 products (+ bf16 output rounding)
+    assert rel_err(outs[0], ref) < tol, rel_err(outs[0], ref)
+    assert rel_err(outs[0], outs[1]) < tol
+
+
 @pytest.mark.parametrize("dt,C,view", [("f32", 64, False), ("bf16", 64, False), ("bf16", 256, False),
                                        ("bf16", 48, True), ("f32", 36, False)])
 def test_se_layer_matches_torch(dt, C, view):
