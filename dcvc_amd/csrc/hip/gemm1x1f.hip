@@ -201,6 +201,176 @@ __global__ void __launch_bounds__(256) gemm1x1f_kernel(GF p) {
   });
 }
 
+// Variant on v_mfma_f32_32x32x2_f32 (64-cycle issue, 16 accumulators per
+// lane): half the MFMA instructions of the 16x16x4 form for the same work and
+// one f32 operand per lane per MFMA.  Both forms are a k-ascending f32 fma
+// chain, so the results are bit-identical.  4 waves in a 2 x 2 grid, each
+// (BM / 2) x (BN / 2) in 32 x 32 MFMA tiles; LDS rows of KK + 1 floats (odd:
+// a 32-lane half reading rows r..r+31 at one k touches 32 banks).
+template <int KK> __host__ __device__ constexpr int ldk32() { return KK + 1; }
+
+template <int BM, int BN, int KK>
+__host__ __device__ constexpr size_t lds_main32() {
+  return (size_t)2 * (BM + BN) * ldk32<KK>() * 4 > (size_t)BM * (BN + 4) * 4 ? (size_t)2 * (BM + BN) * ldk32<KK>() * 4
+                                                                              : (size_t)BM * (BN + 4) * 4;
+}
+
+template <int BM, int BN, int KK>
+__global__ void __launch_bounds__(256) gemm1x1f32_kernel(GF p) {
+  constexpr int kLD = ldk32<KK>();
+  constexpr int Q = KK / 8;
+  constexpr int TM = BM / 64, TN = BN / 64;  // 32x32 tiles per wave
+  constexpr int PX = (BM * Q + 255) / 256;
+  constexpr int PW = (BN * Q + 255) / 256;
+  static_assert(TM >= 1 && TN >= 1, "tile");
+  extern __shared__ __align__(16) unsigned char smem[];
+  float *Xs = reinterpret_cast<float *>(smem);  // [2][BM][kLD]
+  float *Ws = Xs + 2 * BM * kLD;                 // [2][BN][kLD]
+  float *Lc = reinterpret_cast<float *>(smem + lds_main32<BM, BN, KK>());
+
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int wm = wave & 1, wn = wave >> 1;
+  const int tm = blockIdx.x % p.tiles_m, tn = blockIdx.x / p.tiles_m;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int nsteps = (p.wstride + KK - 1) / KK;
+  epi::stage_consts(p, Lc, n0, BN);
+
+  float4 pxa[PX], pxb[PX], pwa[PW], pwb[PW];
+  auto load_step = [&](int s) {
+    const int k0 = s * KK;
+#pragma unroll
+    for (int i = 0; i < PX; ++i) {
+      const int it = threadIdx.x + i * 256;
+      const int r = it / Q, q = it % Q;
+      const int m = m0 + r, c = k0 + q * 8;
+      if (it < BM * Q && m < p.M && c < p.cin) {
+        const float *src = p.x + (int64_t)m * p.xcs + p.xco + c;
+        pxa[i] = *reinterpret_cast<const float4 *>(src);
+        pxb[i] = *reinterpret_cast<const float4 *>(src + 4);
+      } else {
+        pxa[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+        pxb[i] = pxa[i];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < PW; ++i) {
+      const int it = threadIdx.x + i * 256;
+      const int r = it / Q, q = it % Q;
+      const int n = n0 + r, c = k0 + q * 8;
+      if (it < BN * Q && n < p.cout && c < p.wstride) {
+        const float *src = p.w + (int64_t)n * p.wstride + c;
+        pwa[i] = *reinterpret_cast<const float4 *>(src);
+        pwb[i] = *reinterpret_cast<const float4 *>(src + 4);
+      } else {
+        pwa[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+        pwb[i] = pwa[i];
+      }
+    }
+  };
+  auto lrelu4 = [&](float4 v) {
+    const float s = p.in_slope;
+    v.x = v.x >= 0.f ? v.x : v.x * s;
+    v.y = v.y >= 0.f ? v.y : v.y * s;
+    v.z = v.z >= 0.f ? v.z : v.z * s;
+    v.w = v.w >= 0.f ? v.w : v.w * s;
+    return v;
+  };
+  auto put8 = [&](float *d, float4 a, float4 b) {
+    d[0] = a.x; d[1] = a.y; d[2] = a.z; d[3] = a.w;
+    d[4] = b.x; d[5] = b.y; d[6] = b.z; d[7] = b.w;
+  };
+  auto store_step = [&](int buf) {
+    float *xs = Xs + buf * BM * kLD;
+    float *ws = Ws + buf * BN * kLD;
+#pragma unroll
+    for (int i = 0; i < PX; ++i) {
+      const int it = threadIdx.x + i * 256;
+      if (BM * Q % 256 == 0 || it < BM * Q) {
+        const int r = it / Q, q = it % Q;
+        float4 a = pxa[i], b = pxb[i];
+        if (p.in_op == DCVC_IN_LRELU) {
+          a = lrelu4(a);
+          b = lrelu4(b);
+        }
+        put8(xs + r * kLD + q * 8, a, b);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < PW; ++i) {
+      const int it = threadIdx.x + i * 256;
+      if (BN * Q % 256 == 0 || it < BN * Q) {
+        const int r = it / Q, q = it % Q;
+        put8(ws + r * kLD + q * 8, pwa[i], pwb[i]);
+      }
+    }
+  };
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+
+  const int r32 = lane & 31, h = lane >> 5;
+  load_step(0);
+  store_step(0);
+  __syncthreads();
+  for (int s = 0; s < nsteps; ++s) {
+    const int buf = s & 1;
+    if (s + 1 < nsteps) load_step(s + 1);
+    const float *xs = Xs + buf * BM * kLD;
+    const float *ws = Ws + buf * BN * kLD;
+#pragma unroll
+    for (int kk = 0; kk < KK / 2; ++kk) {
+      float a[TN], b[TM];
+#pragma unroll
+      for (int j = 0; j < TN; ++j) a[j] = ws[((wn * TN + j) * 32 + r32) * kLD + 2 * kk + h];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) b[i] = xs[((wm * TM + i) * 32 + r32) * kLD + 2 * kk + h];
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[j], b[i], acc[i][j], 0, 0, 0);
+    }
+    if (s + 1 < nsteps) store_step(buf ^ 1);
+    __syncthreads();
+  }
+
+  float *T = reinterpret_cast<float *>(smem);
+  constexpr int LD = BN + 4;
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        epi::put4(p, T, LD, (wm * TM + i) * 32 + r32, (wn * TN + j) * 32 + 8 * g + 4 * h, Lc,
+                  f32x4{acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2], acc[i][j][4 * g + 3]});
+  __syncthreads();
+  epi::store_tile<float, epi::ipt(BM, BN, 256)>(p, T, LD, BM, n0, min(BN, p.cout - n0), Lc, BN,
+                                                [&](int l, int &oy, int &ox) {
+    const int m = m0 + l;
+    oy = m / p.W;
+    ox = m - oy * p.W;
+    return m < p.M;
+  });
+}
+
+template <int BM, int BN, int KK>
+int launch32(GF p, hipStream_t st) {
+  p.tiles_m = (p.M + BM - 1) / BM;
+  const int tiles_n = (p.cout + BN - 1) / BN;
+  const size_t lds = lds_main32<BM, BN, KK>() + epi::consts_floats(BN) * 4;
+  auto kern = gemm1x1f32_kernel<BM, BN, KK>;
+  dcvc_note_kernel("gemm1x1f32_kernel<%d, %d, %d>@%lld", BM, BN, KK, (long long)p.tiles_m * tiles_n * 256);
+  if (lds > 64 * 1024) dcvc_ensure_lds(reinterpret_cast<const void *>(kern), (int)lds);
+  hipLaunchKernelGGL(kern, dim3((unsigned)(p.tiles_m * tiles_n)), dim3(256), lds, st, p);
+  DCVC_LAUNCH_CHECK();
+  return DCVC_HIP_OK;
+}
+
 template <int BM, int BN, int WMW, int KK>
 int launch(GF p, hipStream_t st) {
   p.tiles_m = (p.M + BM - 1) / BM;
@@ -218,7 +388,8 @@ int g_use_gemm_f32 = 1;
 int g_cfg = 0;  // dcvc_set_option("gemm1x1_f32_cfg", i): force tile config i (A/B), 0 = automatic
 
 // Tile choice, from A/B timings of every configuration on the 68x120 latent
-// shapes (scripts/gemm_f32_bench.py, profiles/r02_gemm_f32.jsonl): 64 x 64
+// shapes (scripts/gemm_f32_bench.py, profiles/r02_gemm_f32.jsonl): 128 x 64
+// tiles on the 32x32x2 form for narrow-in / wide-out layers, 64 x 64
 // tiles with 32-channel steps for Cout >= 256, 64 x 32 tiles with 64-channel
 // steps below (1.2-1.8x over the widest-tile rule at 384->1024, 768->192,
 // 512->128); maps too small to give 512 such workgroups use 32-pixel tiles.
@@ -235,9 +406,15 @@ int dispatch(const GF &p, hipStream_t st) {
     case 9: return launch<32, 128, 1, 32>(p, st);
     case 10: return launch<128, 32, 4, 32>(p, st);
     case 11: return launch<64, 32, 4, 64>(p, st);
+    case 12: return launch32<64, 64, 32>(p, st);
+    case 13: return launch32<128, 64, 32>(p, st);
+    case 14: return launch32<64, 128, 32>(p, st);
+    case 15: return launch32<64, 64, 64>(p, st);
     default: break;
   }
   auto blocks = [&](int bm, int bn) { return (long)((p.M + bm - 1) / bm) * ((p.cout + bn - 1) / bn); };
+  // 32x32x2 MFMA, 128-pixel tiles: 192->768 at 68x120 33 -> 30.5 us
+  if (p.cin <= 256 && p.cout >= 512 && blocks(128, 64) >= 512) return launch32<128, 64, 32>(p, st);
   if (p.cout >= 256 && blocks(64, 64) >= 512) return launch<64, 64, 2, 32>(p, st);
   if (blocks(64, 32) >= 512) return launch<64, 32, 4, 64>(p, st);
   if (p.cout > 32) return launch<32, 64, 2, 32>(p, st);

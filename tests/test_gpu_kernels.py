@@ -317,13 +317,16 @@ def test_gemm1x1_equals_generic_conv(case, xdt):
 @pytest.mark.parametrize("case", [(384, 384, 68, 120), (1024, 384, 17, 30), (384, 1024, 9, 13), (192, 192, 68, 120),
                                   (768, 192, 20, 33), (40, 64, 17, 19), (128, 512, 33, 47), (96, 288, 34, 60),
                                   (64, 2, 8, 9), (104, 16, 5, 7)])
-def test_gemm1x1_f32_equals_generic_conv(case):
-    """The fp32 1x1 GEMM (gemm1x1f.hip) and conv.hip's f32 path run the same
-    exact-f32 MFMA chain (k ascending, 4 per instruction): bit-identical
-    outputs with the lrelu input op, activation, residual and shuffle; and
-    within f32 tolerance of torch."""
+@pytest.mark.parametrize("cfg", [0, 12, 13, 14, 15])
+def test_gemm1x1_f32_equals_generic_conv(case, cfg):
+    """The fp32 1x1 GEMM (gemm1x1f.hip; cfg 0 = automatic tile choice, 12-15
+    force the v_mfma_f32_32x32x2_f32 variants) and conv.hip's f32 path run
+    the same exact-f32 MFMA chain (k ascending): bit-identical outputs with
+    the lrelu input op, activation, residual and shuffle; and within f32
+    tolerance of torch."""
     h = K()
     cin, cout, H, W = case
+    h.set_option("gemm1x1_f32_cfg", cfg)
     x = torch.randn(1, cin, H, W)
     w = torch.randn(cout, cin, 1, 1) / cin ** 0.5
     b = torch.randn(cout) * 0.1
@@ -340,6 +343,7 @@ def test_gemm1x1_f32_equals_generic_conv(case):
         torch.cuda.synchronize()
         outs.append((back(y), back(y1), back(y2)))
     h.set_option("gemm1x1_f32", 1)
+    h.set_option("gemm1x1_f32_cfg", 0)
     for a, c in zip(outs[0], outs[1]):
         assert torch.equal(a, c)
     ref = F.leaky_relu(F.conv2d(F.leaky_relu(x, 0.1), w, b), 0.01) + rt
