@@ -20,6 +20,8 @@ RCCL; no collective touches the per-frame path.  value = frames of all ranks
 import argparse
 import json
 import os
+import sys
+import threading
 import time
 
 import numpy as np
@@ -293,8 +295,22 @@ def pmc_traffic(kname, workload):
     return None
 
 
+def heartbeat(period=60.0):
+    """A line on stderr every `period` seconds while the bench runs (long CPU
+    baseline samples would otherwise look like a hung process to a watchdog
+    that expects output); the JSON result stays the only stdout line."""
+    t0 = time.time()
+
+    def beat():
+        while True:
+            time.sleep(period)
+            print(f"bench: running, {time.time() - t0:.0f} s", file=sys.stderr, flush=True)
+    threading.Thread(target=beat, daemon=True).start()
+
+
 def main():
     args = parse()
+    heartbeat()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
