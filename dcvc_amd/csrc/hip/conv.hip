@@ -525,6 +525,8 @@ extern "C" void dcvc_internal_dcbp_enable(int v);
 extern "C" void dcvc_internal_dcbs_enable(int v);
 extern "C" int dcvc_internal_conv7s(const dcvc_conv_args *a, void *stream);
 extern "C" void dcvc_internal_conv7s_enable(int v);
+extern "C" int dcvc_internal_conv7w(const dcvc_conv_args *a, void *stream);
+extern "C" void dcvc_internal_conv7w_enable(int v);
 extern "C" void dcvc_internal_conv3p_occupancy(int v);
 extern "C" void dcvc_internal_gemm1x1_bm(int v);
 
@@ -592,7 +594,9 @@ extern "C" int dcvc_conv2d(const dcvc_conv_args *a, void *stream) {
     if (r != DCVC_HIP_EUNSUPPORTED) return r;
   }
   if (a->kh == 7 && a->kw == 7 && a->compute == DCVC_BF16) {
-    const int r = dcvc_internal_conv7s(a, stream);   // SpyNet's 8- / 16-channel layers
+    int r = dcvc_internal_conv7s(a, stream);   // SpyNet's 8- / 16-channel layers
+    if (r != DCVC_HIP_EUNSUPPORTED) return r;
+    r = dcvc_internal_conv7w(a, stream);       // and its 32- / 64-channel ones
     if (r != DCVC_HIP_EUNSUPPORTED) return r;
   }
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
@@ -637,6 +641,10 @@ extern "C" int dcvc_set_option(const char *name, int value) {
   }
   if (std::strcmp(name, "dcb_persistent") == 0) {
     dcvc_internal_dcbp_enable(value);
+    return DCVC_HIP_OK;
+  }
+  if (std::strcmp(name, "conv7_wide_cin") == 0) {
+    dcvc_internal_conv7w_enable(value);
     return DCVC_HIP_OK;
   }
   if (std::strcmp(name, "conv7_small_cin") == 0) {

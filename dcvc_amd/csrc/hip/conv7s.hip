@@ -50,7 +50,7 @@ struct G7 {
   static constexpr int TPK = 32 / CIN;               // taps per 32-wide K step
   static constexpr int KS = (49 + TPK - 1) / TPK;    // K steps per window (13 | 25)
   static constexpr int KP = KS * 32;                 // packed K
-  static constexpr int WP = KP + 8;                  // LDS weight row pitch (16-byte skew per row)
+  static constexpr int WP = KP + 16;                 // LDS weight row pitch (32-byte skew per row: conflict-free A reads)
   static constexpr int NT = BN / 16;
   static constexpr int LD = BN + 4;                  // fp32 epilogue tile row
   static constexpr size_t WB = (size_t)BN * WP * 2;

@@ -3,7 +3,7 @@
     python scripts/conv3_bench.py [--reps 30] [--shapes 48x48@1088x1920r,...]
 
 A shape is CINxCOUT@HxW, with a trailing "r" for a bf16 residual input (the
-ResBlock form out = x + conv(...)).  Prints one JSON line per shape: the
+ResBlock form out = x + conv(...)) and / or "k7" for a 7x7 kernel (SpyNet).  Prints one JSON line per shape: the
 kernel, us/launch, algorithmic GB/s (input, weights, output and residual read
 or written once) and TFLOP/s.
 """
@@ -26,11 +26,13 @@ def main():
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
     for sh in a.shapes.split(","):
-        res = sh.endswith("r")
-        ch, hw = sh.rstrip("r").split("@")
+        k = 7 if "k7" in sh else 3
+        base = sh.replace("k7", "")
+        res = base.endswith("r")
+        ch, hw = base.rstrip("r").split("@")
         cin, cout = (int(v) for v in ch.split("x"))
         H, W = (int(v) for v in hw.split("x"))
-        cw = K.ConvW(torch.randn(cout, cin, 3, 3) / (cin * 9) ** 0.5, torch.randn(cout) * 0.1, 1, K.BF16, dev)
+        cw = K.ConvW(torch.randn(cout, cin, k, k) / (cin * k * k) ** 0.5, torch.randn(cout) * 0.1, 1, K.BF16, dev)
         x = K.from_nchw(torch.randn(1, cin, H, W, device=dev), K.BF16)
         r = K.from_nchw(torch.randn(1, cout, H, W, device=dev), K.BF16) if res else None
         y = K.empty(H, W, cout, K.BF16, dev)
@@ -43,9 +45,9 @@ def main():
         e1.record()
         torch.cuda.synchronize()
         us = e0.elapsed_time(e1) * 1e3 / a.reps
-        nb = H * W * 2 * (cin + cout * (2 if res else 1)) + cout * cin * 9 * 2
+        nb = H * W * 2 * (cin + cout * (2 if res else 1)) + cout * cin * k * k * 2
         print(json.dumps({"shape": sh, "kernel": K.lib().dcvc_last_kernel().decode(), "us": round(us, 2),
-                          "gbs": round(nb / us / 1e3, 1), "tflops": round(2.0 * H * W * cin * cout * 9 / us / 1e6, 1)}),
+                          "gbs": round(nb / us / 1e3, 1), "tflops": round(2.0 * H * W * cin * cout * k * k / us / 1e6, 1)}),
               flush=True)
 
 

@@ -617,6 +617,34 @@ def test_conv7_small_cin_matches_torch(cin, cout, H, W, res, out32):
     assert rel_err(outs[0], outs[1]) < tol
 
 
+@pytest.mark.parametrize("cin,cout,H,W", [(32, 64, 272, 480), (64, 32, 272, 480), (32, 16, 272, 480),
+                                         (32, 64, 37, 45), (64, 32, 21, 19), (32, 16, 9, 70)])
+def test_conv7_wide_cin_matches_torch(cin, cout, H, W):
+    """conv7w.hip (SpyNet's 32- and 64-channel 7x7 layers: persistent,
+    resident weights, slot-rotated halo image) vs torch fp32 on the
+    bf16-rounded operands and vs the generic conv.hip path (ReLU, bf16 out)."""
+    h = K()
+    x = torch.randn(1, cin, H, W)
+    w = torch.randn(cout, cin, 7, 7) / (cin * 49) ** 0.5
+    b = torch.randn(cout) * 0.1
+    ref = F.relu(F.conv2d(x.bfloat16().float(), w.bfloat16().float(), b, padding=3))
+    cw = h.ConvW(w, b, 1, h.BF16)
+    xa = to_act(x, h.BF16)
+    outs, names = [], []
+    for on in (1, 0):
+        h.set_option("conv7_wide_cin", on)
+        try:
+            y = h.conv(cw, xa, out_dtype=h.BF16, act=h.ACT_LRELU, slope=0.0)
+        finally:
+            h.set_option("conv7_wide_cin", 1)
+        outs.append(back(y))
+        names.append(h.lib().dcvc_last_kernel().decode())
+    torch.cuda.synchronize()
+    assert names[0].startswith("conv7w_kernel") and names[1].startswith("conv_kernel"), names
+    assert rel_err(outs[0], ref) < 1e-2
+    assert rel_err(outs[0], outs[1]) < 1e-2
+
+
 @pytest.mark.parametrize("dt,C,view", [("f32", 64, False), ("bf16", 64, False), ("bf16", 256, False),
                                        ("bf16", 48, True), ("f32", 36, False)])
 def test_se_layer_matches_torch(dt, C, view):
