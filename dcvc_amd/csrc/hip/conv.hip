@@ -527,6 +527,8 @@ extern "C" int dcvc_internal_conv7s(const dcvc_conv_args *a, void *stream);
 extern "C" void dcvc_internal_conv7s_enable(int v);
 extern "C" int dcvc_internal_conv7w(const dcvc_conv_args *a, void *stream);
 extern "C" void dcvc_internal_conv7w_enable(int v);
+extern "C" int dcvc_internal_conv3s2(const dcvc_conv_args *a, void *stream);
+extern "C" void dcvc_internal_conv3s2_enable(int v);
 extern "C" void dcvc_internal_conv3p_occupancy(int v);
 extern "C" void dcvc_internal_gemm1x1_bm(int v);
 
@@ -593,6 +595,10 @@ extern "C" int dcvc_conv2d(const dcvc_conv_args *a, void *stream) {
     const int r = dcvc_internal_gemm1x1_f32(a, stream);
     if (r != DCVC_HIP_EUNSUPPORTED) return r;
   }
+  if (a->kh == 3 && a->kw == 3 && a->stride == 2 && a->compute == DCVC_BF16) {
+    const int r = dcvc_internal_conv3s2(a, stream);   // downsampling convs, persistent
+    if (r != DCVC_HIP_EUNSUPPORTED) return r;
+  }
   if (a->kh == 7 && a->kw == 7 && a->compute == DCVC_BF16) {
     int r = dcvc_internal_conv7s(a, stream);   // SpyNet's 8- / 16-channel layers
     if (r != DCVC_HIP_EUNSUPPORTED) return r;
@@ -641,6 +647,10 @@ extern "C" int dcvc_set_option(const char *name, int value) {
   }
   if (std::strcmp(name, "dcb_persistent") == 0) {
     dcvc_internal_dcbp_enable(value);
+    return DCVC_HIP_OK;
+  }
+  if (std::strcmp(name, "conv3x3_s2") == 0) {
+    dcvc_internal_conv3s2_enable(value);
     return DCVC_HIP_OK;
   }
   if (std::strcmp(name, "conv7_wide_cin") == 0) {

@@ -645,6 +645,42 @@ def test_conv7_wide_cin_matches_torch(cin, cout, H, W):
     assert rel_err(outs[0], outs[1]) < 1e-2
 
 
+@pytest.mark.parametrize("cin,cout,H,W,res,coff", [(56, 64, 544, 960, False, 0), (48, 64, 545, 961, True, 8),
+                                                   (64, 96, 544, 962, False, 0), (64, 64, 547, 959, True, 0)])
+def test_conv3x3_stride2_persistent_matches_torch(cin, cout, H, W, res, coff):
+    """conv3s2.hip (persistent stride-2 3x3, resident weights, column-
+    de-interleaved input image) vs torch fp32 on the bf16-rounded operands and
+    vs the generic conv.hip path: odd map sizes, an input channel view, the
+    residual epilogue, two n-blocks (96 outputs); maps of >= 2 output tiles
+    per CU (smaller ones take the per-tile kernel)."""
+    h = K()
+    big = torch.randn(1, cin + coff, H, W)
+    x = big[:, coff:coff + cin]
+    w = torch.randn(cout, cin, 3, 3) / (cin * 9) ** 0.5
+    b = torch.randn(cout) * 0.1
+    Ho, Wo = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+    r = torch.randn(1, cout, Ho, Wo) if res else None
+    ref = F.leaky_relu(F.conv2d(x.bfloat16().float(), w.bfloat16().float(), b, stride=2, padding=1), 0.1)
+    if res:
+        ref = ref + r.bfloat16().float()
+    cw = h.ConvW(w, b, 2, h.BF16)
+    xa = to_act(big, h.BF16).ch(coff, cin)
+    ra = to_act(r, h.BF16) if res else None
+    outs, names = [], []
+    for on in (1, 0):
+        h.set_option("conv3x3_s2", on)
+        try:
+            y = h.conv(cw, xa, out_dtype=h.BF16, act=h.ACT_LRELU, slope=0.1, res=ra)
+        finally:
+            h.set_option("conv3x3_s2", 1)
+        outs.append(back(y))
+        names.append(h.lib().dcvc_last_kernel().decode())
+    torch.cuda.synchronize()
+    assert names[0].startswith("conv3s2_kernel") and names[1].startswith("conv_kernel"), names
+    assert rel_err(outs[0], ref) < 1e-2
+    assert rel_err(outs[0], outs[1]) < 1e-2
+
+
 @pytest.mark.parametrize("dt,C,view", [("f32", 64, False), ("bf16", 64, False), ("bf16", 256, False),
                                        ("bf16", 48, True), ("f32", 36, False)])
 def test_se_layer_matches_torch(dt, C, view):
