@@ -56,7 +56,7 @@ __host__ __device__ constexpr size_t lds_main() {
                                                                             : (size_t)BM * (BN + 4) * 4;
 }
 
-template <int BM, int BN, int WMW, int KK>
+template <int BM, int BN, int WMW, int KK, bool LIN>
 __global__ void __launch_bounds__(256) gemm1x1f_kernel(GF p) {
   constexpr int kLD = ldk<KK>();
   constexpr int Q = KK / 8;                 // 8-float pieces per row per step
@@ -127,7 +127,7 @@ __global__ void __launch_bounds__(256) gemm1x1f_kernel(GF p) {
       if (BM * Q % 256 == 0 || it < BM * Q) {
         const int r = it / Q, q = it % Q;
         float4 a = pxa[i], b = pxb[i];
-        if (p.in_op == DCVC_IN_LRELU) {
+        if constexpr (LIN) {  // input op leaky ReLU (a template flag: no run-time branch)
           a = lrelu4(a);
           b = lrelu4(b);
         }
@@ -376,8 +376,10 @@ int launch(GF p, hipStream_t st) {
   p.tiles_m = (p.M + BM - 1) / BM;
   const int tiles_n = (p.cout + BN - 1) / BN;
   const size_t lds = lds_main<BM, BN, KK>() + epi::consts_floats(BN) * 4;
-  auto kern = gemm1x1f_kernel<BM, BN, WMW, KK>;
-  dcvc_note_kernel("gemm1x1f_kernel<%d, %d, %d, %d>@%lld", BM, BN, WMW, KK, (long long)p.tiles_m * tiles_n * 256);
+  const bool lin = p.in_op == DCVC_IN_LRELU;
+  auto kern = lin ? gemm1x1f_kernel<BM, BN, WMW, KK, true> : gemm1x1f_kernel<BM, BN, WMW, KK, false>;
+  dcvc_note_kernel("gemm1x1f_kernel<%d, %d, %d, %d, %s>@%lld", BM, BN, WMW, KK, bname(lin),
+                   (long long)p.tiles_m * tiles_n * 256);
   if (lds > 64 * 1024) dcvc_ensure_lds(reinterpret_cast<const void *>(kern), (int)lds);
   hipLaunchKernelGGL(kern, dim3((unsigned)(p.tiles_m * tiles_n)), dim3(256), lds, st, p);
   DCVC_LAUNCH_CHECK();
