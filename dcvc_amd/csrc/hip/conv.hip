@@ -517,6 +517,7 @@ extern "C" int64_t dcvc_conv_pack_weights(const float *w, int cout, int cin, int
 extern "C" int dcvc_internal_gemm1x1(const dcvc_conv_args *a, void *stream);
 extern "C" int dcvc_internal_gemm1x1_f32(const dcvc_conv_args *a, void *stream);
 extern "C" void dcvc_internal_gemm1x1_f32_enable(int v);
+extern "C" void dcvc_internal_gemm3x3_f32_enable(int v);
 extern "C" void dcvc_internal_gemm1x1_f32_cfg(int v);
 extern "C" int dcvc_internal_conv3x3(const dcvc_conv_args *a, void *stream);
 extern "C" void dcvc_internal_conv3x3_resident(int v);
@@ -591,8 +592,8 @@ extern "C" int dcvc_conv2d(const dcvc_conv_args *a, void *stream) {
     const int r = dcvc_internal_gemm1x1(a, stream);
     if (r != DCVC_HIP_EUNSUPPORTED) return r;
   }
-  if (a->kh == 1 && a->kw == 1 && a->stride == 1 && a->compute == DCVC_F32) {
-    const int r = dcvc_internal_gemm1x1_f32(a, stream);
+  if (((a->kh == 1 && a->kw == 1) || (a->kh == 3 && a->kw == 3)) && a->stride == 1 && a->compute == DCVC_F32) {
+    const int r = dcvc_internal_gemm1x1_f32(a, stream);   // 1x1 and 3x3 (shifted GEMMs) fp32
     if (r != DCVC_HIP_EUNSUPPORTED) return r;
   }
   if (a->kh == 3 && a->kw == 3 && a->stride == 2 && a->compute == DCVC_BF16) {
@@ -635,6 +636,10 @@ extern "C" int dcvc_set_option(const char *name, int value) {
   }
   if (std::strcmp(name, "gemm1x1_f32") == 0) {
     dcvc_internal_gemm1x1_f32_enable(value);
+    return DCVC_HIP_OK;
+  }
+  if (std::strcmp(name, "gemm3x3_f32") == 0) {
+    dcvc_internal_gemm3x3_f32_enable(value);
     return DCVC_HIP_OK;
   }
   if (std::strcmp(name, "gemm1x1_f32_cfg") == 0) {

@@ -56,7 +56,11 @@ __host__ __device__ constexpr size_t lds_main() {
                                                                             : (size_t)BM * (BN + 4) * 4;
 }
 
-template <int BM, int BN, int WMW, int KK, bool LIN>
+// K3: 3x3 stride-1 pad-1 conv as nine shifted 1x1 GEMMs over the same
+// pixel tile: step s = (32-channel chunk s / 9, tap s % 9), the order of
+// conv.hip's f32 path (chunk-major, taps inside), so again bit-identical;
+// the shifted rows of a tap are contiguous in memory (zero outside the map).
+template <int BM, int BN, int WMW, int KK, bool LIN, bool K3 = false>
 __global__ void __launch_bounds__(256) gemm1x1f_kernel(GF p) {
   constexpr int kLD = ldk<KK>();
   constexpr int Q = KK / 8;                 // 8-float pieces per row per step
@@ -77,16 +81,39 @@ __global__ void __launch_bounds__(256) gemm1x1f_kernel(GF p) {
   const int m0 = tm * BM, n0 = tn * BN;
   const int nsteps = (p.wstride + KK - 1) / KK;
   epi::stage_consts(p, Lc, n0, BN);
+  static_assert(!K3 || KK == 32, "3x3: 32-channel steps");
+  const int cinp = K3 ? p.wstride / 9 : 0;
+  int py[PX], px_[PX];   // K3: map coordinates of this thread's staged pixels
+#pragma unroll
+  for (int i = 0; i < PX; ++i) {
+    const int m = m0 + (threadIdx.x + i * 256) / Q;
+    py[i] = m / p.W;
+    px_[i] = m - py[i] * p.W;
+  }
 
   float4 pxa[PX], pxb[PX], pwa[PW], pwb[PW];
   auto load_step = [&](int s) {
-    const int k0 = s * KK;
+    int k0 = s * KK, kw = k0, dy = 0, dx = 0;
+    if constexpr (K3) {
+      const int chunk = s / 9, tap = s - chunk * 9;
+      dy = tap / 3 - 1;
+      dx = tap % 3 - 1;
+      k0 = chunk * 32;
+      kw = tap * cinp + k0;
+    }
 #pragma unroll
     for (int i = 0; i < PX; ++i) {
       const int it = threadIdx.x + i * 256;
       const int r = it / Q, q = it % Q;
-      const int m = m0 + r, c = k0 + q * 8;
-      if (it < BM * Q && m < p.M && c < p.cin) {
+      int m = m0 + r;
+      const int c = k0 + q * 8;
+      bool ok = it < BM * Q && m < p.M && c < p.cin;
+      if constexpr (K3) {
+        const int sy = py[i] + dy, sx = px_[i] + dx;
+        ok = ok && sy >= 0 && sy < p.M / p.W && sx >= 0 && sx < p.W;
+        m = sy * p.W + sx;
+      }
+      if (ok) {
         const float *src = p.x + (int64_t)m * p.xcs + p.xco + c;
         pxa[i] = *reinterpret_cast<const float4 *>(src);
         pxb[i] = *reinterpret_cast<const float4 *>(src + 4);
@@ -99,7 +126,7 @@ __global__ void __launch_bounds__(256) gemm1x1f_kernel(GF p) {
     for (int i = 0; i < PW; ++i) {
       const int it = threadIdx.x + i * 256;
       const int r = it / Q, q = it % Q;
-      const int n = n0 + r, c = k0 + q * 8;
+      const int n = n0 + r, c = kw + q * 8;
       if (it < BN * Q && n < p.cout && c < p.wstride) {
         const float *src = p.w + (int64_t)n * p.wstride + c;
         pwa[i] = *reinterpret_cast<const float4 *>(src);
@@ -371,14 +398,14 @@ int launch32(GF p, hipStream_t st) {
   return DCVC_HIP_OK;
 }
 
-template <int BM, int BN, int WMW, int KK>
+template <int BM, int BN, int WMW, int KK, bool K3 = false>
 int launch(GF p, hipStream_t st) {
   p.tiles_m = (p.M + BM - 1) / BM;
   const int tiles_n = (p.cout + BN - 1) / BN;
   const size_t lds = lds_main<BM, BN, KK>() + epi::consts_floats(BN) * 4;
   const bool lin = p.in_op == DCVC_IN_LRELU;
-  auto kern = lin ? gemm1x1f_kernel<BM, BN, WMW, KK, true> : gemm1x1f_kernel<BM, BN, WMW, KK, false>;
-  dcvc_note_kernel("gemm1x1f_kernel<%d, %d, %d, %d, %s>@%lld", BM, BN, WMW, KK, bname(lin),
+  auto kern = lin ? gemm1x1f_kernel<BM, BN, WMW, KK, true, K3> : gemm1x1f_kernel<BM, BN, WMW, KK, false, K3>;
+  dcvc_note_kernel("gemm1x1f_kernel<%d, %d, %d, %d, %s, %s>@%lld", BM, BN, WMW, KK, bname(lin), bname(K3),
                    (long long)p.tiles_m * tiles_n * 256);
   if (lds > 64 * 1024) dcvc_ensure_lds(reinterpret_cast<const void *>(kern), (int)lds);
   hipLaunchKernelGGL(kern, dim3((unsigned)(p.tiles_m * tiles_n)), dim3(256), lds, st, p);
@@ -387,6 +414,7 @@ int launch(GF p, hipStream_t st) {
 }
 
 int g_use_gemm_f32 = 1;
+int g_use_k3 = 1;   // dcvc_set_option("gemm3x3_f32", 0/1): fp32 3x3 s1 convs as shifted GEMMs (A/B)
 int g_cfg = 0;  // dcvc_set_option("gemm1x1_f32_cfg", i): force tile config i (A/B), 0 = automatic
 
 // Tile choice, from A/B timings of every configuration on the 68x120 latent
@@ -423,13 +451,24 @@ int dispatch(const GF &p, hipStream_t st) {
   return launch<32, 32, 2, 32>(p, st);
 }
 
+// 3x3: 32-channel steps only (the chunk-major K order of conv.hip)
+int dispatch3(const GF &p, hipStream_t st) {
+  auto blocks = [&](int bm, int bn) { return (long)((p.M + bm - 1) / bm) * ((p.cout + bn - 1) / bn); };
+  if (p.cout >= 256 && p.cout % 64 == 0 && blocks(64, 64) >= 512) return launch<64, 64, 2, 32, true>(p, st);
+  if (blocks(64, 32) >= 512) return launch<64, 32, 4, 32, true>(p, st);
+  if (p.cout > 32) return launch<32, 64, 2, 32, true>(p, st);
+  return launch<32, 32, 2, 32, true>(p, st);
+}
+
 }  // namespace
 
 // Called by dcvc_conv2d for 1x1 stride-1 convs with f32 compute, f32 in/out
 // and 32-byte-aligned channel views; returns DCVC_HIP_EUNSUPPORTED otherwise.
 extern "C" int dcvc_internal_gemm1x1_f32(const dcvc_conv_args *a, void *stream) {
-  if (!g_use_gemm_f32) return DCVC_HIP_EUNSUPPORTED;
-  if (a->kh != 1 || a->kw != 1 || a->stride != 1 || a->compute != DCVC_F32) return DCVC_HIP_EUNSUPPORTED;
+  const bool k3 = a->kh == 3 && a->kw == 3 && a->stride == 1 && a->pad == 1;
+  if (!(k3 ? g_use_k3 : g_use_gemm_f32) || a->compute != DCVC_F32) return DCVC_HIP_EUNSUPPORTED;
+  if (!k3 && (a->kh != 1 || a->kw != 1 || a->stride != 1)) return DCVC_HIP_EUNSUPPORTED;
+  if (k3 && a->shuffle) return DCVC_HIP_EUNSUPPORTED;
   if (a->in_op != DCVC_IN_NONE && a->in_op != DCVC_IN_LRELU) return DCVC_HIP_EUNSUPPORTED;
   if (a->x.dtype != DCVC_F32 || a->y.dtype != DCVC_F32) return DCVC_HIP_EUNSUPPORTED;
   if (a->cin % 8 || a->x.cstride % 4 || a->x.coff % 4 || ((uintptr_t)a->x.ptr & 15) || ((uintptr_t)a->w & 15))
@@ -447,7 +486,7 @@ extern "C" int dcvc_internal_gemm1x1_f32(const dcvc_conv_args *a, void *stream) 
   p.yco = a->y.coff;
   p.cin = a->cin;
   p.cout = a->cout;
-  p.wstride = (a->cin + kK - 1) / kK * kK;  // packed row length; steps of KK = 64 read zeros past it
+  p.wstride = (a->cin + kK - 1) / kK * kK * (k3 ? 9 : 1);  // packed row length; steps of KK = 64 read zeros past it
   p.in_op = a->in_op;
   p.in_slope = a->in_slope;
   p.act = a->act;
@@ -469,8 +508,10 @@ extern "C" int dcvc_internal_gemm1x1_f32(const dcvc_conv_args *a, void *stream) 
   if (a->res.ptr) vo = vo && (p.rcs % 8 == 0) && (p.rco % 8 == 0) && (((uintptr_t)p.res & 15) == 0);
   if (a->res2.ptr) vo = vo && (p.r2cs % 8 == 0) && (p.r2co % 8 == 0) && (((uintptr_t)p.res2 & 15) == 0);
   p.vec_out = vo ? 1 : 0;
+  if (k3) return dispatch3(p, reinterpret_cast<hipStream_t>(stream));
   return dispatch(p, reinterpret_cast<hipStream_t>(stream));
 }
 
 extern "C" void dcvc_internal_gemm1x1_f32_enable(int v) { g_use_gemm_f32 = v; }
+extern "C" void dcvc_internal_gemm3x3_f32_enable(int v) { g_use_k3 = v; }
 extern "C" void dcvc_internal_gemm1x1_f32_cfg(int v) { g_cfg = v; }

@@ -351,6 +351,41 @@ def test_gemm1x1_f32_equals_generic_conv(case, cfg):
     assert rel_err(outs[0][1], F.conv2d(x, w, b)) < 2e-5
 
 
+@pytest.mark.parametrize("case", [(384, 288, 68, 120), (480, 384, 34, 60), (192, 192, 17, 30), (40, 64, 17, 19),
+                                  (128, 128, 9, 13), (64, 16, 5, 70)])
+def test_gemm3x3_f32_equals_generic_conv(case):
+    """fp32 3x3 stride-1 convs as nine shifted GEMMs (gemm1x1f.hip, K3) run
+    conv.hip's f32 MFMA chain in its order (32-channel chunk-major, taps
+    inside): bit-identical outputs with the lrelu input op, activation and
+    residual; within f32 tolerance of torch."""
+    h = K()
+    cin, cout, H, W = case
+    x = torch.randn(1, cin, H, W)
+    w = torch.randn(cout, cin, 3, 3) / (cin * 9) ** 0.5
+    b = torch.randn(cout) * 0.1
+    cw = h.ConvW(w, b, 1, h.F32)
+    xa = to_act(x, h.F32)
+    rt = torch.randn(1, cout, H, W)
+    outs, names = [], []
+    for use in (1, 0):
+        h.set_option("gemm3x3_f32", use)
+        try:
+            r = to_act(rt, h.F32)
+            y = h.conv(cw, xa, out_dtype=h.F32, in_op=h.IN_LRELU, in_slope=0.1, act=h.ACT_LRELU, slope=0.01, res=r)
+            names.append(h.lib().dcvc_last_kernel().decode())
+            y1 = h.conv(cw, xa, out_dtype=h.F32)
+            torch.cuda.synchronize()
+            outs.append((back(y), back(y1)))
+        finally:
+            h.set_option("gemm3x3_f32", 1)
+    assert names[0].startswith("gemm1x1f_kernel") and names[1].startswith("conv_kernel"), names
+    for a_, c_ in zip(outs[0], outs[1]):
+        assert torch.equal(a_, c_)
+    ref = F.leaky_relu(F.conv2d(F.leaky_relu(x, 0.1), w, b, padding=1), 0.01) + rt
+    assert rel_err(outs[0][0], ref) < 2e-5
+    assert rel_err(outs[0][1], F.conv2d(x, w, b, padding=1)) < 2e-5
+
+
 C3_CASES = [
     # cin, cout, H, W, coff (input channel view offset in a wider buffer)
     (64, 64, 37, 61, 0), (96, 192, 20, 33, 0), (128, 128, 9, 13, 0), (192, 96, 11, 70, 0),
