@@ -21,8 +21,13 @@
 //   * the tiles of one XCD's workgroups are consecutive in raster order, so
 //     halo rows and columns shared by neighbouring tiles are L2 hits;
 //   * the epilogue is specialised to what these layers need (bias, leaky
-//     ReLU, up to two bf16 residuals, per-channel scale, bf16 store) and
-//     goes through an fp32 LDS tile that reuses the input image's space.
+//     ReLU, up to two bf16 residuals, per-channel scale, bf16 store); for
+//     16-row tiles it runs straight from the accumulators (each lane stores
+//     4 channels of one pixel, residual pieces prefetched a tile ahead in the
+//     same shape), so waves leave a tile without a barrier and, where two
+//     input images fit, tile t + 1 is published while slower waves still
+//     read tile t's: one barrier per tile.  Pixel shuffle and 8-row tiles go
+//     through an fp32 LDS tile that reuses the input image's space.
 // The MFMA sequence (per 32-channel chunk, taps 0..8; then a 16-channel tail
 // as five tap pairs) and the fp32 epilogue order are those of conv3x3.hip, so
 // results are bit-identical to it (tests/test_gpu_kernels.py).
@@ -51,10 +56,11 @@ struct P3 {
   int act;
   float slope;
   int tiles_x, tiles_y, nblk_n;
-  int xbytes, rbytes, r2bytes;
+  int xbytes, rbytes, r2bytes, ybytes;
 };
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 
 // 8-element pieces of the output / residual type; an element index < 0
 // reads zeros (out-of-range buffer offset)
@@ -65,11 +71,11 @@ template <> struct Vec8<uint16_t> {
     return __builtin_bit_cast(u16x8, __builtin_amdgcn_raw_buffer_load_b128(r, e < 0 ? 0x7ffffff0 : e * 2, 0, 0));
   }
   __device__ __forceinline__ static float get(const raw &v, int j) { return bf2f(v[j]); }
-  __device__ __forceinline__ static void store(uint16_t *p, const float v[8]) {
+  __device__ __forceinline__ static void bstore(__amdgpu_buffer_rsrc_t r, int e, const float v[8]) {
     u16x8 o;
 #pragma unroll
     for (int j = 0; j < 8; ++j) o[j] = f2bf(v[j]);
-    *reinterpret_cast<u16x8 *>(p) = o;
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o), r, e < 0 ? 0x7ffffff0 : e * 2, 0, 0);
   }
 };
 typedef float f32x8 __attribute__((ext_vector_type(8)));
@@ -83,9 +89,10 @@ template <> struct Vec8<float> {
     return f32x8{fa[0], fa[1], fa[2], fa[3], fb[0], fb[1], fb[2], fb[3]};
   }
   __device__ __forceinline__ static float get(const raw &v, int j) { return v[j]; }
-  __device__ __forceinline__ static void store(float *p, const float v[8]) {
-    *reinterpret_cast<float4 *>(p) = make_float4(v[0], v[1], v[2], v[3]);
-    *reinterpret_cast<float4 *>(p + 4) = make_float4(v[4], v[5], v[6], v[7]);
+  __device__ __forceinline__ static void bstore(__amdgpu_buffer_rsrc_t r, int e, const float v[8]) {
+    const int o = e < 0 ? 0x7fffffe0 : e * 4;
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, f32x4{v[0], v[1], v[2], v[3]}), r, o, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, f32x4{v[4], v[5], v[6], v[7]}), r, o + 16, 0, 0);
   }
 };
 
@@ -93,7 +100,11 @@ __device__ __forceinline__ int swz(int row, int x, int slot) {
   return row * 32 + ((slot ^ (((x >> 2) & 1) << 1)) << 3);
 }
 
-template <int CIN, int BN, int NW, int RW>
+// MODE 0: epilogue through an fp32 LDS tile (pixel shuffle), one input
+// image; 1: epilogue straight from the accumulators, one image; 2: direct
+// epilogue, two images (tile t + 1 is published while slower waves still
+// read tile t's, so one barrier per tile)
+template <int CIN, int BN, int NW, int RW, int MODE = 0>
 struct Geo {
   static constexpr int NCH = CIN / 32;
   static constexpr bool TAIL = (CIN % 32) == 16;
@@ -108,9 +119,10 @@ struct Geo {
   static constexpr int LD = BN + 4;                       // fp32 epilogue tile row
   static constexpr size_t TB = (size_t)TH * 16 * LD * 4;
   static constexpr size_t IB = (size_t)NIMG * IMG * 2;
-  static constexpr size_t BUF = IB > TB ? IB : TB;
+  static constexpr size_t BUF = MODE == 2 ? 2 * IB : MODE == 1 ? IB : (IB > TB ? IB : TB);
   static constexpr size_t LC = WB + BUF;                  // bias | scale
-  static constexpr size_t LDS = LC + 2 * BN * 4;
+  static constexpr size_t DUMMY = LC + 2 * BN * 4;        // 16-byte sink for idle staging lanes
+  static constexpr size_t LDS = DUMMY + 16;
   static constexpr int QP = CIN / 8;                      // 16-byte pieces per pixel
   static constexpr int PIX = IH * 18;
   static constexpr int PP = (PIX * QP + NTHR - 1) / NTHR; // input pieces per thread
@@ -118,9 +130,11 @@ struct Geo {
   static constexpr int PO = (TH * 16 * OQ + NTHR - 1) / NTHR;  // output pieces per thread (either layout)
 };
 
-template <int CIN, int BN, int NW, int RW, typename TOUT, bool SHUF>
+template <int CIN, int BN, int NW, int RW, typename TOUT, bool SHUF, int MODE>
 __global__ void __launch_bounds__(NW * 64) conv3p_kernel(P3 p) {
-  typedef Geo<CIN, BN, NW, RW> G_;
+  static_assert(!SHUF || MODE == 0, "pixel shuffle goes through the LDS tile");
+  typedef Geo<CIN, BN, NW, RW, MODE> G_;
+  constexpr bool kDirect = MODE != 0;
   constexpr int NCH = G_::NCH, KS = G_::KS, NT = G_::NT, TH = G_::TH, IMG = G_::IMG;
   constexpr int NTHR = G_::NTHR, QP = G_::QP, PP = G_::PP, LD = G_::LD, OQ = G_::OQ, PO = G_::PO;
   constexpr int ROWB = kPitch * 32;
@@ -129,6 +143,7 @@ __global__ void __launch_bounds__(NW * 64) conv3p_kernel(P3 p) {
   uint16_t *Li = reinterpret_cast<uint16_t *>(smem + G_::WB);
   float *T = reinterpret_cast<float *>(smem + G_::WB);
   float *Lc = reinterpret_cast<float *>(smem + G_::LC);
+  uint16_t *const Ldummy = reinterpret_cast<uint16_t *>(smem + G_::DUMMY);
 
   const int tid = threadIdx.x;
   const int wave = tid >> 6, lane = tid & 63;
@@ -160,8 +175,11 @@ __global__ void __launch_bounds__(NW * 64) conv3p_kernel(P3 p) {
     }
   }
   // buffer loads: an out-of-range offset returns zeros, so halo pixels outside
-  // the image need no branch (a branch around each load makes hipcc wait for
-  // it on the spot, which would serialise the prefetch)
+  // the image (and tiles past the last) need no branch.  Every global load and
+  // store in the tile loop is unconditional and every loaded value is
+  // consumed unconditionally: hipcc's s_waitcnt placement counts outstanding
+  // memory operations per path, and one conditional load or store makes it
+  // fall back to vmcnt(0), which waits for the prefetch two tiles ahead too.
   const __amdgpu_buffer_rsrc_t xr =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t *>(p.x), (short)0, p.xbytes, 0x00020000);
   auto issue = [&](int t, u16x8 (&pf)[PP]) {
@@ -176,23 +194,21 @@ __global__ void __launch_bounds__(NW * 64) conv3p_kernel(P3 p) {
       pf[u] = __builtin_bit_cast(u16x8, v);
     }
   };
-  auto publish = [&](const u16x8 (&pf)[PP]) {
+  auto publish = [&](const u16x8 (&pf)[PP], uint16_t *Li) {
     if (p.in_lrelu) {
 #pragma unroll
       for (int u = 0; u < PP; ++u) {
-        if (lofs[u] < 0) continue;
         u16x8 v = pf[u];
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const float f = bf2f(v[j]);
           v[j] = f2bf(f >= 0.f ? f : f * p.in_slope);
         }
-        *reinterpret_cast<u16x8 *>(Li + lofs[u]) = v;
+        *reinterpret_cast<u16x8 *>(lofs[u] >= 0 ? Li + lofs[u] : Ldummy) = v;
       }
     } else {
 #pragma unroll
-      for (int u = 0; u < PP; ++u)
-        if (lofs[u] >= 0) *reinterpret_cast<u16x8 *>(Li + lofs[u]) = pf[u];
+      for (int u = 0; u < PP; ++u) *reinterpret_cast<u16x8 *>(lofs[u] >= 0 ? Li + lofs[u] : Ldummy) = pf[u];
     }
   };
 
@@ -203,7 +219,7 @@ __global__ void __launch_bounds__(NW * 64) conv3p_kernel(P3 p) {
   constexpr bool kDeep = RW == 2;
   u16x8 pfa[PP], pfb[PP];
   issue(g, pfa);
-  if (kDeep && g + G < ntiles) issue(g + G, pfb);
+  if constexpr (kDeep) issue(g + G, pfb);
   // ---- resident weights [KS][BN][32] (swizzled by row) + epilogue constants
   for (int it = tid; it < KS * BN * 4; it += NTHR) {
     const int row = it >> 2, sl = it & 3;
@@ -246,6 +262,7 @@ __global__ void __launch_bounds__(NW * 64) conv3p_kernel(P3 p) {
       __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p.res), (short)0, p.rbytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t rr2 =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p.res2), (short)0, p.r2bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t yr = __builtin_amdgcn_make_buffer_rsrc(p.y, (short)0, p.ybytes, 0x00020000);
 
   // epilogue-B piece u of tile t: 8 consecutive output channels of one
   // output pixel, in output-row order (SHUF: conv channel n of pixel (y, x)
@@ -286,24 +303,55 @@ __global__ void __launch_bounds__(NW * 64) conv3p_kernel(P3 p) {
       bool ok;
       piece(t, u, ob, src, cq, ok);
       const int cb = (SHUF ? n0 / 4 : n0) + cq;
-      if (p.res) r1[u] = Vec8<TOUT>::load(rr, ok ? (int)(ob * p.rcs + p.rco + cb) : -1);
-      if (p.res2) r2[u] = Vec8<TOUT>::load(rr2, ok ? (int)(ob * p.r2cs + p.r2co + cb) : -1);
+      r1[u] = Vec8<TOUT>::load(rr, ok ? (int)(ob * p.rcs + p.rco + cb) : -1);  // no residual: 0-byte buffer
+      r2[u] = Vec8<TOUT>::load(rr2, ok ? (int)(ob * p.r2cs + p.r2co + cb) : -1);
     }
   };
-  RV ra1[PO], ra2[PO];
-  load_res(g, ra1, ra2);
+  // MODE != 0: residual pieces are the accumulators' own (4 channels of one
+  // pixel per lane and (row, n-tile)), 8 (bf16) or 16 (f32) bytes each
+  typedef typename std::conditional<sizeof(TOUT) == 2, u16x4, f32x4>::type DV;
+  auto dload = [&](__amdgpu_buffer_rsrc_t r, int e) -> DV {
+    if constexpr (sizeof(TOUT) == 2) {
+      return __builtin_bit_cast(u16x4, __builtin_amdgcn_raw_buffer_load_b64(r, e < 0 ? 0x7ffffff0 : e * 2, 0, 0));
+    } else {
+      return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, e < 0 ? 0x7ffffff0 : e * 4, 0, 0));
+    }
+  };
+  auto dget = [](const DV &v, int e) -> float {
+    if constexpr (sizeof(TOUT) == 2) return bf2f(v[e]);
+    else return v[e];
+  };
+  auto load_dres = [&](int t, DV (&d1)[RW][NT], DV (&d2)[RW][NT]) {
+    const int oy0 = (t / p.tiles_x) * TH, ox0 = (t % p.tiles_x) * 16;
+    const int ox = ox0 + col;
+#pragma unroll
+    for (int r = 0; r < RW; ++r) {
+      const int oy = oy0 + wave * RW + r;
+      const bool ok = oy < p.H && ox < p.W;
+      const int ob = oy * p.Wout + ox;
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+        const int n = n0 + j * 16 + hi * 4;
+        d1[r][j] = dload(rr, ok ? ob * p.rcs + p.rco + n : -1);     // no residual: 0-byte buffer
+        d2[r][j] = dload(rr2, ok ? ob * p.r2cs + p.r2co + n : -1);
+      }
+    }
+  };
+  RV ra1[kDirect ? 1 : PO], ra2[kDirect ? 1 : PO];
+  DV da1[kDirect ? RW : 1][NT], da2[kDirect ? RW : 1][NT];
+  if constexpr (kDirect) load_dres(g, da1, da2);
+  else load_res(g, ra1, ra2);
+  int ib = 0;  // MODE 2: image buffer of the current tile
 
   // one tile; returns whether this workgroup has a next one
-  auto tile = [&](int t, u16x8 (&pf)[PP], RV (&r1)[PO], RV (&r2)[PO]) -> bool {
-    publish(pf);
+  auto tile = [&](int t, u16x8 (&pf)[PP], RV (&r1)[kDirect ? 1 : PO], RV (&r2)[kDirect ? 1 : PO],
+                  DV (&d1)[kDirect ? RW : 1][NT], DV (&d2)[kDirect ? RW : 1][NT]) -> bool {
+    uint16_t *const Lt = Li + (MODE == 2 ? ib * (G_::NIMG * IMG) : 0);
+    publish(pf, Lt);
     __syncthreads();
     const int tn = t + G;
     const bool more = tn < ntiles;
-    if (kDeep) {
-      if (tn + G < ntiles) issue(tn + G, pf);  // in flight across the next two tiles
-    } else if (more) {
-      issue(tn, pf);
-    }
+    issue(kDeep ? tn + G : tn, pf);  // kDeep: in flight across the next two tiles
 
     f32x4 acc[RW][NT];
 #pragma unroll
@@ -321,7 +369,7 @@ __global__ void __launch_bounds__(NW * 64) conv3p_kernel(P3 p) {
           a[j] = *reinterpret_cast<const bf16x8 *>(LwA + ((c * 9 + k) * BN + j * 16) * 32);
 #pragma unroll
         for (int r = 0; r < RW; ++r)
-          b[r] = *reinterpret_cast<const bf16x8 *>(Li + c * IMG + offB[dx] + (r + dy) * ROWB);
+          b[r] = *reinterpret_cast<const bf16x8 *>(Lt + c * IMG + offB[dx] + (r + dy) * ROWB);
 #pragma unroll
         for (int r = 0; r < RW; ++r)
 #pragma unroll
@@ -337,7 +385,7 @@ __global__ void __launch_bounds__(NW * 64) conv3p_kernel(P3 p) {
         for (int j = 0; j < NT; ++j)
           a[j] = *reinterpret_cast<const bf16x8 *>(LwA + ((9 * NCH + pr) * BN + j * 16) * 32);
 #pragma unroll
-        for (int r = 0; r < RW; ++r) b[r] = *reinterpret_cast<const bf16x8 *>(Li + offT[pr] + r * ROWB);
+        for (int r = 0; r < RW; ++r) b[r] = *reinterpret_cast<const bf16x8 *>(Lt + offT[pr] + r * ROWB);
 #pragma unroll
         for (int r = 0; r < RW; ++r)
 #pragma unroll
@@ -345,6 +393,58 @@ __global__ void __launch_bounds__(NW * 64) conv3p_kernel(P3 p) {
             acc[r][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[j], b[r], acc[r][j], 0, 0, 0);
       }
     }
+    if constexpr (kDirect) {
+      // ---- epilogue straight from the accumulators: out = scale * (res2 +
+      // (res + act(acc + bias))), the fp32 operations and order of the LDS
+      // tile path (bit-identical); lane stores 4 channels of one pixel
+      const int oy0 = (t / p.tiles_x) * TH, ox = (t % p.tiles_x) * 16 + col;
+#pragma unroll
+      for (int r = 0; r < RW; ++r) {
+        const int oy = oy0 + wave * RW + r;
+        const bool ok = oy < p.H && ox < p.W;
+        const int yb = (oy * p.Wout + ox) * p.ycs + p.yco + n0;  // element offset (< 2^31 / 4, checked on the host)
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+          const int nl = j * 16 + hi * 4;
+          const float4 bb = *reinterpret_cast<const float4 *>(Lc + nl);
+          float v[4] = {acc[r][j][0] + bb.x, acc[r][j][1] + bb.y, acc[r][j][2] + bb.z, acc[r][j][3] + bb.w};
+          if (p.act == DCVC_ACT_LRELU) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = v[e] >= 0.f ? v[e] : v[e] * p.slope;
+          }
+          if (p.res) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = dget(d1[r][j], e) + v[e];
+          }
+          if (p.res2) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = dget(d2[r][j], e) + v[e];
+          }
+          if (p.scale) {
+            const float4 sc = *reinterpret_cast<const float4 *>(Lc + BN + nl);
+            v[0] *= sc.x;
+            v[1] *= sc.y;
+            v[2] *= sc.z;
+            v[3] *= sc.w;
+          }
+          // out-of-range pixels: an out-of-range offset drops the store
+          const int so = ok ? (yb + nl) * (int)sizeof(TOUT) : 0x7ffffff0;
+          if constexpr (sizeof(TOUT) == 2) {
+            u16x4 o;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) o[e] = f2bf(v[e]);
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, o), yr, so, 0, 0);
+          } else {
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, f32x4{v[0], v[1], v[2], v[3]}), yr, so, 0, 0);
+          }
+        }
+      }
+      if (!more) return false;
+      load_dres(tn, d1, d2);  // the next tile's residual pieces
+      if constexpr (MODE == 1) __syncthreads();  // image read by every wave before the next publish
+      if constexpr (MODE == 2) ib ^= 1;
+      return true;
+    } else {
     __syncthreads();  // every wave is done reading the image: T may overwrite it
 
     // ---- epilogue A: v = act(acc + bias) -> fp32 tile T[pixel][LD]
@@ -378,7 +478,7 @@ __global__ void __launch_bounds__(NW * 64) conv3p_kernel(P3 p) {
         int src, cq;
         bool ok;
         piece(t, u, ob, src, cq, ok);
-        if (!ok) continue;
+        src = ok ? src : 0;  // keep idle lanes' tile reads in range
         float v[8];
         if constexpr (SHUF) {
 #pragma unroll
@@ -401,18 +501,20 @@ __global__ void __launch_bounds__(NW * 64) conv3p_kernel(P3 p) {
 #pragma unroll
           for (int j = 0; j < 8; ++j) v[j] = v[j] * Lc[BN + cq + j];
         }
-        Vec8<TOUT>::store(reinterpret_cast<TOUT *>(p.y) + ob * p.ycs + p.yco + (SHUF ? n0 / 4 : n0) + cq, v);
+        // pieces outside the map or past the tile plan: an out-of-range offset drops the store
+        Vec8<TOUT>::bstore(yr, ok ? (int)(ob * p.ycs + p.yco + (SHUF ? n0 / 4 : n0) + cq) : -1, v);
       }
     }
     if (!more) return false;
     load_res(tn, r1, r2);   // the next tile's residual pieces, in flight during its publish and MFMAs
     __syncthreads();  // T read by every thread before the next image overwrites it
     return true;
+    }
   };
   for (int t = g;;) {
-    if (!tile(t, pfa, ra1, ra2)) break;
+    if (!tile(t, pfa, ra1, ra2, da1, da2)) break;
     t += G;
-    if (!tile(t, kDeep ? pfb : pfa, ra1, ra2)) break;
+    if (!tile(t, kDeep ? pfb : pfa, ra1, ra2, da1, da2)) break;
     t += G;
   }
 }
@@ -420,10 +522,11 @@ __global__ void __launch_bounds__(NW * 64) conv3p_kernel(P3 p) {
 int g_cus = 0;
 int g_enabled = 1;
 int g_occ = 1;  // dcvc_set_option("conv3x3_occupancy", 2): two 8-row workgroups per CU where they fit
+int g_mode = 0;  // dcvc_set_option("conv3x3_epilogue", 0/1/2, 3 = also 8-row tiles): highest epilogue mode (launch_mode)
 
-template <int CIN, int BN, int NW, int RW, typename TOUT, bool SHUF>
+template <int CIN, int BN, int NW, int RW, typename TOUT, bool SHUF, int MODE>
 int launch(P3 p, hipStream_t st, int per_cu = 1) {
-  typedef Geo<CIN, BN, NW, RW> G_;
+  typedef Geo<CIN, BN, NW, RW, MODE> G_;
   if constexpr (G_::LDS > 160 * 1024) {
     return DCVC_HIP_EUNSUPPORTED;
   } else {
@@ -443,9 +546,9 @@ int launch(P3 p, hipStream_t st, int per_cu = 1) {
     int64_t G = (int64_t)g_cus * per_cu / p.nblk_n;
     if (G > ntiles) G = ntiles;
     if (G < 1) G = 1;
-    auto kern = conv3p_kernel<CIN, BN, NW, RW, TOUT, SHUF>;
-    dcvc_note_kernel("conv3p_kernel<%d, %d, %d, %d, %s, %s>@%lld", CIN, BN, NW, RW, tname<TOUT>(), bname(SHUF),
-                     (long long)G * p.nblk_n * NW * 64);
+    auto kern = conv3p_kernel<CIN, BN, NW, RW, TOUT, SHUF, MODE>;
+    dcvc_note_kernel("conv3p_kernel<%d, %d, %d, %d, %s, %s, %d>@%lld", CIN, BN, NW, RW, tname<TOUT>(), bname(SHUF),
+                     MODE, (long long)G * p.nblk_n * NW * 64);
     dcvc_ensure_lds(reinterpret_cast<const void *>(kern), (int)G_::LDS);
     hipLaunchKernelGGL(kern, dim3((unsigned)(G * p.nblk_n)), dim3(NW * 64), G_::LDS, st, p);
     DCVC_LAUNCH_CHECK();
@@ -453,14 +556,35 @@ int launch(P3 p, hipStream_t st, int per_cu = 1) {
   }
 }
 
+// Epilogue / image mode for layers without pixel shuffle, at most g_mode
+// (dcvc_set_option("conv3x3_epilogue", m), A/B): 2 when two input images fit
+// in the LDS beside the weights, else 1 (0: the fp32 LDS tile).  8-row tiles
+// at one workgroup per CU keep the LDS tile (128->64 at 544x960: 128.5 us vs
+// 133.4 direct); 16-row tiles gain (48->48 at 1080p: 206.5 -> 173.7 us,
+// 96->48 261.7 -> 238.0, 64->64 241.9 -> 232.3; conv3_bench, same box).
+template <int CIN, int BN, int NW, int RW, typename TOUT, bool SHUF>
+int launch_mode(const P3 &p, hipStream_t st, int per_cu) {
+  constexpr size_t cap = 160 * 1024;
+  if constexpr (!SHUF) {
+    if (RW == 1 && per_cu == 1 && g_mode < 3) return launch<CIN, BN, NW, RW, TOUT, SHUF, 0>(p, st, per_cu);
+    if constexpr (Geo<CIN, BN, NW, RW, 2>::LDS * 1 <= cap) {
+      if (g_mode >= 2 && Geo<CIN, BN, NW, RW, 2>::LDS * per_cu <= cap) return launch<CIN, BN, NW, RW, TOUT, SHUF, 2>(p, st, per_cu);
+    }
+    if constexpr (Geo<CIN, BN, NW, RW, 1>::LDS <= cap) {
+      if (g_mode >= 1 && Geo<CIN, BN, NW, RW, 1>::LDS * per_cu <= cap) return launch<CIN, BN, NW, RW, TOUT, SHUF, 1>(p, st, per_cu);
+    }
+  }
+  return launch<CIN, BN, NW, RW, TOUT, SHUF, 0>(p, st, per_cu);
+}
+
 // 16 output rows per tile (8 waves x 2) when the LDS holds it, else 8.
 template <int CIN, int BN, typename TOUT, bool SHUF>
 int pick_th(const P3 &p, hipStream_t st) {
-  if constexpr (2 * Geo<CIN, BN, 8, 1>::LDS <= 160 * 1024) {
-    if (g_occ >= 2) return launch<CIN, BN, 8, 1, TOUT, SHUF>(p, st, 2);
+  if constexpr (2 * Geo<CIN, BN, 8, 1, SHUF ? 0 : 1>::LDS <= 160 * 1024) {
+    if (g_occ >= 2) return launch_mode<CIN, BN, 8, 1, TOUT, SHUF>(p, st, 2);
   }
-  if constexpr (Geo<CIN, BN, 8, 2>::LDS <= 160 * 1024) return launch<CIN, BN, 8, 2, TOUT, SHUF>(p, st);
-  return launch<CIN, BN, 8, 1, TOUT, SHUF>(p, st);
+  if constexpr (Geo<CIN, BN, 8, 2, SHUF ? 0 : 1>::LDS <= 160 * 1024) return launch_mode<CIN, BN, 8, 2, TOUT, SHUF>(p, st, 1);
+  return launch_mode<CIN, BN, 8, 1, TOUT, SHUF>(p, st, 1);
 }
 
 // BN: 64 / 48 / 32 output channels per workgroup (a multiple of 32 with
@@ -531,6 +655,7 @@ extern "C" int dcvc_internal_conv3p(const dcvc_conv_args *a, void *stream) {
     p.r2bytes = a->res2.H * a->res2.W * a->res2.cstride * ye;
   }
   p.xbytes = a->x.H * a->x.W * a->x.cstride * 2;
+  p.ybytes = a->y.H * a->y.W * a->y.cstride * ye;
   p.cout = a->cout;
   p.in_lrelu = a->in_op == DCVC_IN_LRELU;
   p.in_slope = a->in_slope;
@@ -552,3 +677,4 @@ extern "C" int dcvc_internal_conv3p(const dcvc_conv_args *a, void *stream) {
 // dcvc_set_option("conv3x3_persistent", 0/1) (A/B switch, via conv.hip)
 extern "C" void dcvc_internal_conv3p_enable(int v) { g_enabled = v; }
 extern "C" void dcvc_internal_conv3p_occupancy(int v) { g_occ = v; }
+extern "C" void dcvc_internal_conv3p_mode(int v) { g_mode = v; }

@@ -20,11 +20,15 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=30)
     ap.add_argument("--shapes", default="48x48@1088x1920r,64x64@544x960r,96x96@272x480r")
+    ap.add_argument("--opt", action="append", default=[], help="NAME=VALUE for dcvc_set_option (repeatable)")
     a = ap.parse_args()
     import torch
     from dcvc_amd import hip as K
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
+    for o in a.opt:
+        name, val = o.split("=")
+        K.set_option(name, int(val))
     for sh in a.shapes.split(","):
         k = 7 if "k7" in sh else 3
         base = sh.replace("k7", "")
@@ -46,7 +50,7 @@ def main():
         torch.cuda.synchronize()
         us = e0.elapsed_time(e1) * 1e3 / a.reps
         nb = H * W * 2 * (cin + cout * (2 if res else 1)) + cout * cin * k * k * 2
-        print(json.dumps({"shape": sh, "kernel": K.lib().dcvc_last_kernel().decode(), "us": round(us, 2),
+        print(json.dumps({"shape": sh, "opt": a.opt, "kernel": K.lib().dcvc_last_kernel().decode(), "us": round(us, 2),
                           "gbs": round(nb / us / 1e3, 1), "tflops": round(2.0 * H * W * cin * cout * k * k / us / 1e6, 1)}),
               flush=True)
 

@@ -26,11 +26,15 @@ def main():
     ap.add_argument("--W", type=int, default=120)
     ap.add_argument("--k3", action="store_true", help="time HEM's fp32 3x3 latent convs (conv.hip f32 path) instead")
     ap.add_argument("--shapes", default="", help="cin x cout list, e.g. 384x384,1024x384")
+    ap.add_argument("--opt", action="append", default=[], help="NAME=VALUE for dcvc_set_option (repeatable)")
     a = ap.parse_args()
     import torch
     from dcvc_amd import hip as K
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
+    for o in a.opt:
+        name, val = o.split("=")
+        K.set_option(name, int(val))
     rows = []
     k = 3 if a.k3 else 1
     shapes = [(384, 288), (480, 384), (192, 192), (288, 288), (128, 128), (64, 64)] if a.k3 else SHAPES

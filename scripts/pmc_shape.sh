@@ -1,0 +1,25 @@
+#!/bin/bash
+# SQ / LDS / MFMA counters of one conv3_bench shape, one counter group per
+# rocprofv3 pass, summarised per kernel by scripts/pmc_table.py.
+#   bash scripts/pmc_shape.sh 48x48@1088x1920r gpurun_out/pmc48 [--opt name=value ...]
+set -u
+cd "$(dirname "$0")/.."
+export TMPDIR=/tmp
+shape=$1; out=$2; shift 2
+mkdir -p "$out"
+passes=(
+  "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS"
+  "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_SALU SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE"
+  "FETCH_SIZE"
+  "WRITE_SIZE"
+)
+i=0
+for ctr in "${passes[@]}"; do
+  timeout -s KILL 120 rocprofv3 --pmc $ctr -d "$out/p$i" -o run --output-format csv \
+    -- python scripts/conv3_bench.py --reps 5 --shapes "$shape" "$@" > "$out/p$i.log" 2>&1
+  rc=$?
+  echo "pass $i rc=$rc"
+  case $rc in 0) ;; *) tail -5 "$out/p$i.log"; exit $rc ;; esac
+  i=$((i+1))
+done
+python scripts/pmc_table.py "$out"

@@ -450,14 +450,18 @@ P3_CASES = [
 ]
 
 
+@pytest.mark.parametrize("emode", [3, 2, 1, 0])
 @pytest.mark.parametrize("case", P3_CASES)
-def test_conv3x3_persistent_kernel(case):
+def test_conv3x3_persistent_kernel(case, emode):
     """The persistent resident-weight 3x3 kernel (conv3x3p.hip) is
     bit-identical to the per-workgroup kernel (same K order, same fp32
     epilogue order) with every epilogue option on: lrelu input, bias +
     lrelu, two residuals, per-channel scale, ragged image edges, a channel
-    view of a wider input."""
+    view of a wider input; in each epilogue mode (2: straight from the
+    accumulators with two input images, 1: one image, 0: the fp32 LDS
+    tile, 3: mode 2 also for 8-row tiles)."""
     h = K()
+    h.set_option("conv3x3_epilogue", emode)
     cin, cout, H, W, coff = case
     x = torch.randn(1, cin + coff + 8, H, W)
     w = torch.randn(cout, cin, 3, 3) / (9 * cin) ** 0.5
@@ -489,8 +493,11 @@ def test_conv3x3_persistent_kernel(case):
         outs.append(got)
     h.set_option("conv3x3_persistent", 1)
     h.set_option("conv3x3_resident", 1)
+    h.set_option("conv3x3_epilogue", 2)
     k = len(names) // 2
     assert all(n.startswith("conv3p_kernel") for n in names[:k]), names
+    if emode == 0:
+        assert all(n.split(">")[0].endswith(", 0") for n in names[:k]), names
     assert not any(n.startswith("conv3p_kernel") for n in names[k:]), names
     for a, b_ in zip(outs[0], outs[1]):
         assert torch.equal(a, b_)
