@@ -61,11 +61,16 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16,
                     help="host threads for the cpu_baseline oracle run (capped at the cores this process may use)")
+    ap.add_argument("--cpu-baseline-workers", type=int, default=0,
+                    help="only measure the oracle in the reference's worker-per-core mode with this many "
+                         "single-thread workers (no GPU); prints the record profiles/cpu_baseline_workers.json holds")
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--profile-out", default="", help="per-shape kernel timing JSON of one P-frame")
     a = ap.parse_args()
     if a.yuv420 and a.model != "dc":
         ap.error("--yuv420 is the DCVC-DC YUV path (config C4)")
+    if a.cpu_baseline_workers and a.model != "dc":
+        ap.error("--cpu-baseline-workers measures the DCVC-DC oracle")
     if a.height is None:
         a.height = 2160 if a.yuv420 else 1080
     if a.width is None:
@@ -140,17 +145,14 @@ def host_info():
     return {"nproc": os.cpu_count() or 1, "usable": usable, "cpu": model}
 
 
-def cpu_baseline(isd, psd, args):
-    """Oracle (PyTorch fp32 CPU restatement, pinned to the reference) timed on
-    this host: one full-size I-frame and one full-size P-frame (1088x1920 for
-    C3), each compress + rANS encode + rANS decode + decompress in write mode,
-    in one process on `threads` cores; fps = the GOP average
-    gop / (t_I + (gop - 1) t_P).  No area scaling."""
+def oracle_ip_times(isd, psd, args, threads):
+    """(t_I, t_P) seconds of the oracle (PyTorch fp32 CPU restatement, pinned
+    to the reference) on one full-size I-frame and one full-size P-frame
+    (1088x1920 for C3), each compress + rANS encode + rANS decode +
+    decompress in write mode, on `threads` torch threads."""
     from oracle import dc_oracle as O
     from oracle import rans_oracle as R
     from dcvc_amd.synth import moving_pattern, moving_pattern_yuv420, to_float
-    info = host_info()
-    threads = max(1, min(args.cpu_threads, info["usable"]))
     torch.set_num_threads(threads)
     h, w = args.height, args.width
     Hp, Wp = (h + 15) // 16 * 16, (w + 15) // 16 * 16
@@ -193,13 +195,75 @@ def cpu_baseline(isd, psd, args):
         dec = code(pnet.compress(frames[1], dpb, False, args.q_index, 1), "p_")
         pnet.decompress(dpb, dec, h, w, False, args.q_index, 1)
         t_p = time.time() - t0
+    return t_i, t_p
+
+
+def cpu_baseline(isd, psd, args):
+    """The oracle timed on this host in one process on `threads` cores: one
+    full-size I-frame and one full-size P-frame; fps = the GOP average
+    gop / (t_I + (gop - 1) t_P).  No area scaling.  The reference's own
+    worker-per-core mode is measured separately (``--cpu-baseline-workers``)
+    and attached as ``workers`` when its committed record exists."""
+    info = host_info()
+    threads = max(1, min(args.cpu_threads, info["usable"]))
+    h, w = args.height, args.width
+    Hp, Wp = (h + 15) // 16 * 16, (w + 15) // 16 * 16
+    t_i, t_p = oracle_ip_times(isd, psd, args, threads)
     gop = args.gop
     fps = gop / (t_i + (gop - 1) * t_p)
     return {"value": fps, "unit": "frames/s", "cores": threads, "kind": "port",
             "sample": f"oracle write-mode encode+decode of one full-size I-frame ({t_i:.1f} s) and one full-size "
                       f"P-frame ({t_p:.1f} s) at {Hp}x{Wp}, {threads} torch threads in one process; fps = GOP "
                       f"{gop} average; host nproc {info['nproc']}, usable {info['usable']}, CPU {info['cpu']}",
-            "ms_I": round(t_i * 1e3, 1), "ms_P": round(t_p * 1e3, 1)}
+            "ms_I": round(t_i * 1e3, 1), "ms_P": round(t_p * 1e3, 1),
+            **({"workers": _workers_record(args)} if _workers_record(args) else {})}
+
+
+WORKERS_RECORD = os.path.join(HERE, "profiles", "cpu_baseline_workers.json")
+
+
+def _workers_record(args):
+    """The committed worker-per-core measurement of this workload, if any."""
+    try:
+        with open(WORKERS_RECORD) as f:
+            rec = json.load(f)
+    except (OSError, ValueError):
+        return None
+    return rec if rec.get("workload") == [args.model, args.height, args.width, bool(args.yuv420)] else None
+
+
+def _worker(job):
+    isd, psd, args = job
+    return oracle_ip_times(isd, psd, args, 1)
+
+
+def cpu_baseline_workers(args):
+    """The reference's own CPU deployment, DCVC-DC/test_video.py:276-290: a
+    pool of `workers` processes with torch.set_num_threads(1) each, every
+    worker coding its own sequence; here each worker codes one full-size
+    I-frame and one full-size P-frame.  fps = workers x gop / (t_I + (gop - 1)
+    t_P) with each worker's own times (mean), i.e. all workers' frames over
+    the wall time of a GOP.  Runs without touching the GPU (a separate
+    invocation: ``python bench.py --cpu-baseline-workers N``)."""
+    import multiprocessing as mp
+    info = host_info()
+    n = args.cpu_baseline_workers
+    isd, psd = make_weights(None, 0, torch.device("cpu"), args.model)
+    t0 = time.time()
+    with mp.get_context("spawn").Pool(n) as pool:
+        times = pool.map(_worker, [(isd, psd, args)] * n)
+    wall = time.time() - t0
+    t_i = float(np.mean([t[0] for t in times]))
+    t_p = float(np.mean([t[1] for t in times]))
+    fps = n * args.gop / (t_i + (args.gop - 1) * t_p)
+    rec = {"value": fps, "unit": "frames/s", "cores": n, "kind": "port",
+           "workload": [args.model, args.height, args.width, bool(args.yuv420)],
+           "sample": f"{n} worker processes x 1 torch thread (DCVC-DC/test_video.py:276-290), each coding one "
+                     f"full-size I-frame (mean {t_i:.1f} s) and one full-size P-frame (mean {t_p:.1f} s) in write "
+                     f"mode; fps = workers x GOP {args.gop} / (t_I + {args.gop - 1} t_P); wall {wall:.0f} s; host "
+                     f"nproc {info['nproc']}, usable {info['usable']}, CPU {info['cpu']}",
+           "ms_I": [round(t[0] * 1e3, 1) for t in times], "ms_P": [round(t[1] * 1e3, 1) for t in times]}
+    print(json.dumps(rec), flush=True)
 
 
 def hem_q(sd_i, sd_p, rate):
@@ -257,7 +321,55 @@ def cpu_baseline_hem(isd, psd, args):
                       f"full-size P-frame ({t_p:.1f} s) at {Hp}x{Wp}, {threads} torch threads in one process; "
                       f"fps = GOP {gop} average; host nproc {info['nproc']}, usable {info['usable']}, "
                       f"CPU {info['cpu']}",
-            "ms_I": round(t_i * 1e3, 1), "ms_P": round(t_p * 1e3, 1)}
+            "ms_I": round(t_i * 1e3, 1), "ms_P": round(t_p * 1e3, 1),
+            **({"workers": _workers_record(args)} if _workers_record(args) else {})}
+
+
+WORKERS_RECORD = os.path.join(HERE, "profiles", "cpu_baseline_workers.json")
+
+
+def _workers_record(args):
+    """The committed worker-per-core measurement of this workload, if any."""
+    try:
+        with open(WORKERS_RECORD) as f:
+            rec = json.load(f)
+    except (OSError, ValueError):
+        return None
+    return rec if rec.get("workload") == [args.model, args.height, args.width, bool(args.yuv420)] else None
+
+
+def _worker(job):
+    isd, psd, args = job
+    return oracle_ip_times(isd, psd, args, 1)
+
+
+def cpu_baseline_workers(args):
+    """The reference's own CPU deployment, DCVC-DC/test_video.py:276-290: a
+    pool of `workers` processes with torch.set_num_threads(1) each, every
+    worker coding its own sequence; here each worker codes one full-size
+    I-frame and one full-size P-frame.  fps = workers x gop / (t_I + (gop - 1)
+    t_P) with each worker's own times (mean), i.e. all workers' frames over
+    the wall time of a GOP.  Runs without touching the GPU (a separate
+    invocation: ``python bench.py --cpu-baseline-workers N``)."""
+    import multiprocessing as mp
+    info = host_info()
+    n = args.cpu_baseline_workers
+    isd, psd = make_weights(None, 0, torch.device("cpu"), args.model)
+    t0 = time.time()
+    with mp.get_context("spawn").Pool(n) as pool:
+        times = pool.map(_worker, [(isd, psd, args)] * n)
+    wall = time.time() - t0
+    t_i = float(np.mean([t[0] for t in times]))
+    t_p = float(np.mean([t[1] for t in times]))
+    fps = n * args.gop / (t_i + (args.gop - 1) * t_p)
+    rec = {"value": fps, "unit": "frames/s", "cores": n, "kind": "port",
+           "workload": [args.model, args.height, args.width, bool(args.yuv420)],
+           "sample": f"{n} worker processes x 1 torch thread (DCVC-DC/test_video.py:276-290), each coding one "
+                     f"full-size I-frame (mean {t_i:.1f} s) and one full-size P-frame (mean {t_p:.1f} s) in write "
+                     f"mode; fps = workers x GOP {args.gop} / (t_I + {args.gop - 1} t_P); wall {wall:.0f} s; host "
+                     f"nproc {info['nproc']}, usable {info['usable']}, CPU {info['cpu']}",
+           "ms_I": [round(t[0] * 1e3, 1) for t in times], "ms_P": [round(t[1] * 1e3, 1) for t in times]}
+    print(json.dumps(rec), flush=True)
 
 
 def workload_key(argv):
@@ -311,6 +423,8 @@ def heartbeat(period=60.0):
 def main():
     args = parse()
     heartbeat()
+    if args.cpu_baseline_workers:
+        return cpu_baseline_workers(args)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
