@@ -519,6 +519,8 @@ extern "C" int dcvc_internal_gemm1x1_f32(const dcvc_conv_args *a, void *stream);
 extern "C" void dcvc_internal_gemm1x1_f32_enable(int v);
 extern "C" void dcvc_internal_gemm3x3_f32_enable(int v);
 extern "C" void dcvc_internal_gemm1x1_f32_cfg(int v);
+extern "C" void dcvc_internal_gemm1x1_f32_upfront(int v);
+extern "C" void dcvc_internal_gemm1x1_f32_direct(int v);
 extern "C" int dcvc_internal_conv3x3(const dcvc_conv_args *a, void *stream);
 extern "C" void dcvc_internal_conv3x3_resident(int v);
 extern "C" void dcvc_internal_conv3p_enable(int v);
@@ -645,6 +647,14 @@ extern "C" int dcvc_set_option(const char *name, int value) {
   }
   if (std::strcmp(name, "gemm1x1_f32_cfg") == 0) {
     dcvc_internal_gemm1x1_f32_cfg(value);
+    return DCVC_HIP_OK;
+  }
+  if (std::strcmp(name, "gemm1x1_f32_upfront") == 0) {
+    dcvc_internal_gemm1x1_f32_upfront(value);
+    return DCVC_HIP_OK;
+  }
+  if (std::strcmp(name, "gemm1x1_f32_direct") == 0) {
+    dcvc_internal_gemm1x1_f32_direct(value);
     return DCVC_HIP_OK;
   }
   if (std::strcmp(name, "conv3x3") == 0) {

@@ -56,11 +56,66 @@ __host__ __device__ constexpr size_t lds_main() {
                                                                             : (size_t)BM * (BN + 4) * 4;
 }
 
+// Direct epilogue of a wave's TM x TN 16x16 accumulator tiles: tile (i, j)
+// holds, per lane, local channels nl + 16 j .. + 3 of pixel m + 16 i.
+// out = scale * (res2 + (res + act(acc + bias))), epilogue.h's order.  Every
+// residual load is issued before the first store (vmcnt is in order).  The
+// host takes this path only when cout is a multiple of 16, every view is
+// 16-byte aligned (vec_out) and there is no shuffle.
+template <int TM, int TN, int BN>
+__device__ __forceinline__ void direct_epilogue(const GF &p, const f32x4 (&acc)[TM][TN], const float *Lc, int m,
+                                                int n0, int nl) {
+  f32x4 r1[TM][TN], r2[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int mm = m + 16 * i, n = n0 + nl + 16 * j;
+      const bool ok = mm < p.M && n < p.cout;
+      if (p.res && ok) r1[i][j] = *reinterpret_cast<const f32x4 *>(reinterpret_cast<const float *>(p.res) +
+                                                                      (int64_t)mm * p.rcs + p.rco + n);
+      if (p.res2 && ok) r2[i][j] = *reinterpret_cast<const f32x4 *>(reinterpret_cast<const float *>(p.res2) +
+                                                                       (int64_t)mm * p.r2cs + p.r2co + n);
+    }
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int mm = m + 16 * i, n = n0 + nl + 16 * j, c = nl + 16 * j;
+      if (!(mm < p.M && n < p.cout)) continue;
+      const float4 b = *reinterpret_cast<const float4 *>(Lc + c);
+      f32x4 v;
+      v[0] = apply_act(p.act, acc[i][j][0] + b.x, p.slope);
+      v[1] = apply_act(p.act, acc[i][j][1] + b.y, p.slope);
+      v[2] = apply_act(p.act, acc[i][j][2] + b.z, p.slope);
+      v[3] = apply_act(p.act, acc[i][j][3] + b.w, p.slope);
+      if (p.res) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = r1[i][j][e] + v[e];
+      }
+      if (p.res2) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = r2[i][j][e] + v[e];
+      }
+      if (p.scale) {
+        const float4 sc = *reinterpret_cast<const float4 *>(Lc + BN + c);  // stage_consts: scales at Lc + BN
+        v[0] = v[0] * sc.x;
+        v[1] = v[1] * sc.y;
+        v[2] = v[2] * sc.z;
+        v[3] = v[3] * sc.w;
+      }
+      *reinterpret_cast<f32x4 *>(reinterpret_cast<float *>(p.y) + (int64_t)mm * p.ycs + p.yco + n) = v;
+    }
+}
+
 // K3: 3x3 stride-1 pad-1 conv as nine shifted 1x1 GEMMs over the same
 // pixel tile: step s = (32-channel chunk s / 9, tap s % 9), the order of
 // conv.hip's f32 path (chunk-major, taps inside), so again bit-identical;
 // the shifted rows of a tap are contiguous in memory (zero outside the map).
-template <int BM, int BN, int WMW, int KK, bool LIN, bool K3 = false>
+int g_upfront = 1;  // dcvc_set_option("gemm1x1_f32_upfront", 0/1): step operands read up front (A/B)
+int g_direct = 1;   // dcvc_set_option("gemm1x1_f32_direct", 0/1): epilogue straight from the accumulators (A/B)
+
+template <int BM, int BN, int WMW, int KK, bool LIN, bool K3 = false, bool kUpfront = true, bool kDirect = false>
 __global__ void __launch_bounds__(256) gemm1x1f_kernel(GF p) {
   constexpr int kLD = ldk<KK>();
   constexpr int Q = KK / 8;                 // 8-float pieces per row per step
@@ -194,6 +249,26 @@ __global__ void __launch_bounds__(256) gemm1x1f_kernel(GF p) {
     if (s + 1 < nsteps) load_step(s + 1);
     const float *xs = Xs + buf * BM * kLD;
     const float *ws = Ws + buf * BN * kLD;
+    if constexpr (kUpfront) {
+      // every operand of the step read up front (KK / 4 * (TN + TM) VGPRs):
+      // the LDS reads stream back to back and the MFMAs issue without
+      // waiting on a read issued one MFMA earlier
+      float a[KK / 4][TN], b[KK / 4][TM];
+#pragma unroll
+      for (int g = 0; g < KK / 4; ++g) {
+#pragma unroll
+        for (int j = 0; j < TN; ++j) a[g][j] = ws[((wn * TN + j) * 16 + col) * kLD + g * 4 + hi];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) b[g][i] = xs[((wm * TM + i) * 16 + col) * kLD + g * 4 + hi];
+      }
+#pragma unroll
+      for (int g = 0; g < KK / 4; ++g)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[g][j], b[g][i], acc[i][j], 0, 0, 0);
+    } else {
 #pragma unroll
     for (int g = 0; g < KK / 4; ++g) {
       float a[TN], b[TM];
@@ -207,10 +282,19 @@ __global__ void __launch_bounds__(256) gemm1x1f_kernel(GF p) {
         for (int j = 0; j < TN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[j], b[i], acc[i][j], 0, 0, 0);
     }
+    }
     if (s + 1 < nsteps) store_step(buf ^ 1);
     __syncthreads();
   }
 
+  if constexpr (kDirect) {
+    // straight from the accumulators (no shuffle, 16-byte aligned fp32 views,
+    // output pixel = input pixel): a lane holds channels n..n+3 of pixel m
+    // (16x16x4 D layout), one 16-byte residual load and store each; the
+    // operations and their order are epilogue.h's, so results are identical
+    direct_epilogue<TM, TN, BN>(p, acc, Lc, m0 + wm * TM * 16 + col, n0, (wn * TN) * 16 + hi * 4);
+    return;
+  }
   float *T = reinterpret_cast<float *>(smem);
   constexpr int LD = BN + 4;
 #pragma unroll
@@ -242,7 +326,7 @@ __host__ __device__ constexpr size_t lds_main32() {
                                                                               : (size_t)BM * (BN + 4) * 4;
 }
 
-template <int BM, int BN, int KK>
+template <int BM, int BN, int KK, bool kUpfront = true>
 __global__ void __launch_bounds__(256) gemm1x1f32_kernel(GF p) {
   constexpr int kLD = ldk32<KK>();
   constexpr int Q = KK / 8;
@@ -349,6 +433,23 @@ __global__ void __launch_bounds__(256) gemm1x1f32_kernel(GF p) {
     if (s + 1 < nsteps) load_step(s + 1);
     const float *xs = Xs + buf * BM * kLD;
     const float *ws = Ws + buf * BN * kLD;
+    if constexpr (kUpfront) {
+      float a[KK / 2][TN], b[KK / 2][TM];  // the step's operands up front (gemm1x1f_kernel)
+#pragma unroll
+      for (int kk = 0; kk < KK / 2; ++kk) {
+#pragma unroll
+        for (int j = 0; j < TN; ++j) a[kk][j] = ws[((wn * TN + j) * 32 + r32) * kLD + 2 * kk + h];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) b[kk][i] = xs[((wm * TM + i) * 32 + r32) * kLD + 2 * kk + h];
+      }
+#pragma unroll
+      for (int kk = 0; kk < KK / 2; ++kk)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[kk][j], b[kk][i], acc[i][j], 0, 0, 0);
+    } else {
 #pragma unroll
     for (int kk = 0; kk < KK / 2; ++kk) {
       float a[TN], b[TM];
@@ -360,6 +461,7 @@ __global__ void __launch_bounds__(256) gemm1x1f32_kernel(GF p) {
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[j], b[i], acc[i][j], 0, 0, 0);
+    }
     }
     if (s + 1 < nsteps) store_step(buf ^ 1);
     __syncthreads();
@@ -390,8 +492,8 @@ int launch32(GF p, hipStream_t st) {
   p.tiles_m = (p.M + BM - 1) / BM;
   const int tiles_n = (p.cout + BN - 1) / BN;
   const size_t lds = lds_main32<BM, BN, KK>() + epi::consts_floats(BN) * 4;
-  auto kern = gemm1x1f32_kernel<BM, BN, KK>;
-  dcvc_note_kernel("gemm1x1f32_kernel<%d, %d, %d>@%lld", BM, BN, KK, (long long)p.tiles_m * tiles_n * 256);
+  auto kern = g_upfront ? gemm1x1f32_kernel<BM, BN, KK, true> : gemm1x1f32_kernel<BM, BN, KK, false>;
+  dcvc_note_kernel("gemm1x1f32_kernel<%d, %d, %d, %s>@%lld", BM, BN, KK, bname(g_upfront), (long long)p.tiles_m * tiles_n * 256);
   if (lds > 64 * 1024) dcvc_ensure_lds(reinterpret_cast<const void *>(kern), (int)lds);
   hipLaunchKernelGGL(kern, dim3((unsigned)(p.tiles_m * tiles_n)), dim3(256), lds, st, p);
   DCVC_LAUNCH_CHECK();
@@ -404,9 +506,16 @@ int launch(GF p, hipStream_t st) {
   const int tiles_n = (p.cout + BN - 1) / BN;
   const size_t lds = lds_main<BM, BN, KK>() + epi::consts_floats(BN) * 4;
   const bool lin = p.in_op == DCVC_IN_LRELU;
-  auto kern = lin ? gemm1x1f_kernel<BM, BN, WMW, KK, true, K3> : gemm1x1f_kernel<BM, BN, WMW, KK, false, K3>;
-  dcvc_note_kernel("gemm1x1f_kernel<%d, %d, %d, %d, %s, %s>@%lld", BM, BN, WMW, KK, bname(lin), bname(K3),
-                   (long long)p.tiles_m * tiles_n * 256);
+  // direct epilogue (A/B: dcvc_set_option("gemm1x1_f32_direct", 0/1)): no
+  // shuffle, whole 16-channel blocks, 16-byte aligned views
+  const bool direct = g_direct && !p.shuffle && p.vec_out && p.cout % 16 == 0;
+  typedef void (*KF)(GF);
+  KF kern;
+  if (direct) kern = lin ? gemm1x1f_kernel<BM, BN, WMW, KK, true, K3, true, true> : gemm1x1f_kernel<BM, BN, WMW, KK, false, K3, true, true>;
+  else if (g_upfront) kern = lin ? gemm1x1f_kernel<BM, BN, WMW, KK, true, K3, true> : gemm1x1f_kernel<BM, BN, WMW, KK, false, K3, true>;
+  else kern = lin ? gemm1x1f_kernel<BM, BN, WMW, KK, true, K3, false> : gemm1x1f_kernel<BM, BN, WMW, KK, false, K3, false>;
+  dcvc_note_kernel("gemm1x1f_kernel<%d, %d, %d, %d, %s, %s, %s, %s>@%lld", BM, BN, WMW, KK, bname(lin), bname(K3),
+                   bname(direct || g_upfront), bname(direct), (long long)p.tiles_m * tiles_n * 256);
   if (lds > 64 * 1024) dcvc_ensure_lds(reinterpret_cast<const void *>(kern), (int)lds);
   hipLaunchKernelGGL(kern, dim3((unsigned)(p.tiles_m * tiles_n)), dim3(256), lds, st, p);
   DCVC_LAUNCH_CHECK();
@@ -515,3 +624,5 @@ extern "C" int dcvc_internal_gemm1x1_f32(const dcvc_conv_args *a, void *stream) 
 extern "C" void dcvc_internal_gemm1x1_f32_enable(int v) { g_use_gemm_f32 = v; }
 extern "C" void dcvc_internal_gemm3x3_f32_enable(int v) { g_use_k3 = v; }
 extern "C" void dcvc_internal_gemm1x1_f32_cfg(int v) { g_cfg = v; }
+extern "C" void dcvc_internal_gemm1x1_f32_upfront(int v) { g_upfront = v; }
+extern "C" void dcvc_internal_gemm1x1_f32_direct(int v) { g_direct = v; }

@@ -317,33 +317,44 @@ def test_gemm1x1_equals_generic_conv(case, xdt):
 @pytest.mark.parametrize("case", [(384, 384, 68, 120), (1024, 384, 17, 30), (384, 1024, 9, 13), (192, 192, 68, 120),
                                   (768, 192, 20, 33), (40, 64, 17, 19), (128, 512, 33, 47), (96, 288, 34, 60),
                                   (64, 2, 8, 9), (104, 16, 5, 7)])
-@pytest.mark.parametrize("cfg", [0, 12, 13, 14, 15])
-def test_gemm1x1_f32_equals_generic_conv(case, cfg):
+@pytest.mark.parametrize("cfg,upfront,direct", [(0, 1, 1), (0, 1, 0), (0, 0, 0), (8, 1, 1), (12, 1, 1), (13, 1, 1),
+                                                (13, 0, 1), (14, 1, 1), (15, 1, 1)])
+def test_gemm1x1_f32_equals_generic_conv(case, cfg, upfront, direct):
     """The fp32 1x1 GEMM (gemm1x1f.hip; cfg 0 = automatic tile choice, 12-15
-    force the v_mfma_f32_32x32x2_f32 variants) and conv.hip's f32 path run
+    force the v_mfma_f32_32x32x2_f32 variants; upfront 1 / 0 = a step's LDS
+    operands read up front / per MFMA group; direct 1 / 0 = epilogue from the
+    accumulators / through the LDS tile) and conv.hip's f32 path run
     the same exact-f32 MFMA chain (k ascending): bit-identical outputs with
     the lrelu input op, activation, residual and shuffle; and within f32
     tolerance of torch."""
     h = K()
     cin, cout, H, W = case
     h.set_option("gemm1x1_f32_cfg", cfg)
+    h.set_option("gemm1x1_f32_upfront", upfront)
+    h.set_option("gemm1x1_f32_direct", direct)
     x = torch.randn(1, cin, H, W)
     w = torch.randn(cout, cin, 1, 1) / cin ** 0.5
     b = torch.randn(cout) * 0.1
     cw = h.ConvW(w, b, 1, h.F32)
     xa = to_act(x, h.F32)
     rt = torch.randn(1, cout, H, W)
+    rt2 = torch.randn(1, cout, H, W)
+    sc = (torch.rand(cout) + 0.5).cuda()
     outs = []
     for use in (1, 0):
         h.set_option("gemm1x1_f32", use)
         r = to_act(rt, h.F32)
+        r2 = to_act(rt2, h.F32)
         y = h.conv(cw, xa, out_dtype=h.F32, in_op=h.IN_LRELU, in_slope=0.1, act=h.ACT_LRELU, slope=0.01, res=r)
         y1 = h.conv(cw, xa, out_dtype=h.F32)
         y2 = h.conv(cw, xa, shuffle=True, out_dtype=h.F32) if cout % 4 == 0 else y1
+        y3 = h.conv(cw, xa, out_dtype=h.F32, act=h.ACT_LRELU, slope=0.1, res=r, res2=r2, scale=sc)
         torch.cuda.synchronize()
-        outs.append((back(y), back(y1), back(y2)))
+        outs.append((back(y), back(y1), back(y2), back(y3)))
     h.set_option("gemm1x1_f32", 1)
     h.set_option("gemm1x1_f32_cfg", 0)
+    h.set_option("gemm1x1_f32_upfront", 1)
+    h.set_option("gemm1x1_f32_direct", 1)
     for a, c in zip(outs[0], outs[1]):
         assert torch.equal(a, c)
     ref = F.leaky_relu(F.conv2d(F.leaky_relu(x, 0.1), w, b), 0.01) + rt
