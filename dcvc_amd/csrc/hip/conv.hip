@@ -534,6 +534,7 @@ extern "C" int dcvc_internal_conv3s2(const dcvc_conv_args *a, void *stream);
 extern "C" void dcvc_internal_conv3s2_enable(int v);
 extern "C" void dcvc_internal_conv3p_occupancy(int v);
 extern "C" void dcvc_internal_conv3p_mode(int v);
+extern "C" void dcvc_internal_conv3p_rows4(int v);
 extern "C" void dcvc_internal_gemm1x1_bm(int v);
 
 extern "C" int dcvc_conv2d(const dcvc_conv_args *a, void *stream) {
@@ -707,6 +708,10 @@ extern "C" int dcvc_set_option(const char *name, int value) {
   }
   if (std::strcmp(name, "conv3x3_epilogue") == 0) {
     dcvc_internal_conv3p_mode(value);
+    return DCVC_HIP_OK;
+  }
+  if (std::strcmp(name, "conv3x3_rows4") == 0) {
+    dcvc_internal_conv3p_rows4(value);
     return DCVC_HIP_OK;
   }
   return DCVC_HIP_EINVAL;

@@ -295,7 +295,11 @@ __global__ void __launch_bounds__(NW * 64) conv3p_kernel(P3 p) {
   // consumed its own, so their HBM latency hides behind tile t's publish and
   // MFMAs
   typedef typename Vec8<TOUT>::raw RV;
-  auto load_res = [&](int t, RV (&r1)[PO], RV (&r2)[PO]) {
+  // 32-row tiles (RW = 4) take no second residual (the host routes such
+  // layers to 16-row tiles): its pieces would not fit the register budget
+  constexpr bool kR2 = RW != 4;
+  constexpr int PO2 = kR2 ? PO : 1;
+  auto load_res = [&](int t, RV (&r1)[PO], RV (&r2)[PO2]) {
 #pragma unroll
     for (int u = 0; u < PO; ++u) {
       int64_t ob;
@@ -304,7 +308,7 @@ __global__ void __launch_bounds__(NW * 64) conv3p_kernel(P3 p) {
       piece(t, u, ob, src, cq, ok);
       const int cb = (SHUF ? n0 / 4 : n0) + cq;
       r1[u] = Vec8<TOUT>::load(rr, ok ? (int)(ob * p.rcs + p.rco + cb) : -1);  // no residual: 0-byte buffer
-      r2[u] = Vec8<TOUT>::load(rr2, ok ? (int)(ob * p.r2cs + p.r2co + cb) : -1);
+      if constexpr (kR2) r2[u] = Vec8<TOUT>::load(rr2, ok ? (int)(ob * p.r2cs + p.r2co + cb) : -1);
     }
   };
   // MODE != 0: residual pieces are the accumulators' own (4 channels of one
@@ -337,14 +341,14 @@ __global__ void __launch_bounds__(NW * 64) conv3p_kernel(P3 p) {
       }
     }
   };
-  RV ra1[kDirect ? 1 : PO], ra2[kDirect ? 1 : PO];
+  RV ra1[kDirect ? 1 : PO], ra2[kDirect ? 1 : PO2];
   DV da1[kDirect ? RW : 1][NT], da2[kDirect ? RW : 1][NT];
   if constexpr (kDirect) load_dres(g, da1, da2);
   else load_res(g, ra1, ra2);
   int ib = 0;  // MODE 2: image buffer of the current tile
 
   // one tile; returns whether this workgroup has a next one
-  auto tile = [&](int t, u16x8 (&pf)[PP], RV (&r1)[kDirect ? 1 : PO], RV (&r2)[kDirect ? 1 : PO],
+  auto tile = [&](int t, u16x8 (&pf)[PP], RV (&r1)[kDirect ? 1 : PO], RV (&r2)[kDirect ? 1 : PO2],
                   DV (&d1)[kDirect ? RW : 1][NT], DV (&d2)[kDirect ? RW : 1][NT]) -> bool {
     uint16_t *const Lt = Li + (MODE == 2 ? ib * (G_::NIMG * IMG) : 0);
     publish(pf, Lt);
@@ -493,9 +497,11 @@ __global__ void __launch_bounds__(NW * 64) conv3p_kernel(P3 p) {
 #pragma unroll
           for (int j = 0; j < 8; ++j) v[j] = Vec8<TOUT>::get(r1[u], j) + v[j];
         }
-        if (p.res2) {
+        if constexpr (kR2) {
+          if (p.res2) {
 #pragma unroll
-          for (int j = 0; j < 8; ++j) v[j] = Vec8<TOUT>::get(r2[u], j) + v[j];
+            for (int j = 0; j < 8; ++j) v[j] = Vec8<TOUT>::get(r2[u], j) + v[j];
+          }
         }
         if (p.scale) {
 #pragma unroll
@@ -522,6 +528,7 @@ __global__ void __launch_bounds__(NW * 64) conv3p_kernel(P3 p) {
 int g_cus = 0;
 int g_enabled = 1;
 int g_occ = 1;  // dcvc_set_option("conv3x3_occupancy", 2): two 8-row workgroups per CU where they fit
+int g_rows4 = 1;  // dcvc_set_option("conv3x3_rows4", 0/1): 32-row tiles where they fit (A/B; 48->48 at 1080p 176 -> 172 us, 32->32 81 -> 69)
 int g_mode = 0;  // dcvc_set_option("conv3x3_epilogue", 0/1/2, 3 = also 8-row tiles): highest epilogue mode (launch_mode)
 
 template <int CIN, int BN, int NW, int RW, typename TOUT, bool SHUF, int MODE>
@@ -580,6 +587,12 @@ int launch_mode(const P3 &p, hipStream_t st, int per_cu) {
 // 16 output rows per tile (8 waves x 2) when the LDS holds it, else 8.
 template <int CIN, int BN, typename TOUT, bool SHUF>
 int pick_th(const P3 &p, hipStream_t st) {
+  // 32-row tiles (4 rows per wave) where the LDS holds them (A/B: option
+  // "conv3x3_rows4"): 7 LDS operand reads per 12 MFMAs instead of 5 per 6,
+  // 34 / 32 halo rows instead of 18 / 16, half the tiles' fixed work
+  if constexpr (!SHUF && Geo<CIN, BN, 8, 4, 0>::LDS <= 160 * 1024) {
+    if (g_rows4 && !p.res2) return launch<CIN, BN, 8, 4, TOUT, SHUF, 0>(p, st, 1);
+  }
   if constexpr (2 * Geo<CIN, BN, 8, 1, SHUF ? 0 : 1>::LDS <= 160 * 1024) {
     if (g_occ >= 2) return launch_mode<CIN, BN, 8, 1, TOUT, SHUF>(p, st, 2);
   }
@@ -678,3 +691,4 @@ extern "C" int dcvc_internal_conv3p(const dcvc_conv_args *a, void *stream) {
 extern "C" void dcvc_internal_conv3p_enable(int v) { g_enabled = v; }
 extern "C" void dcvc_internal_conv3p_occupancy(int v) { g_occ = v; }
 extern "C" void dcvc_internal_conv3p_mode(int v) { g_mode = v; }
+extern "C" void dcvc_internal_conv3p_rows4(int v) { g_rows4 = v; }

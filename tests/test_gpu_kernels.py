@@ -461,18 +461,20 @@ P3_CASES = [
 ]
 
 
-@pytest.mark.parametrize("emode", [3, 2, 1, 0])
+@pytest.mark.parametrize("emode,rows4", [(3, 0), (2, 0), (1, 0), (0, 0), (0, 1)])
 @pytest.mark.parametrize("case", P3_CASES)
-def test_conv3x3_persistent_kernel(case, emode):
+def test_conv3x3_persistent_kernel(case, emode, rows4):
     """The persistent resident-weight 3x3 kernel (conv3x3p.hip) is
     bit-identical to the per-workgroup kernel (same K order, same fp32
     epilogue order) with every epilogue option on: lrelu input, bias +
     lrelu, two residuals, per-channel scale, ragged image edges, a channel
     view of a wider input; in each epilogue mode (2: straight from the
     accumulators with two input images, 1: one image, 0: the fp32 LDS
-    tile, 3: mode 2 also for 8-row tiles)."""
+    tile, 3: mode 2 also for 8-row tiles); rows4: 32-row tiles where they
+    fit (calls without a second residual)."""
     h = K()
     h.set_option("conv3x3_epilogue", emode)
+    h.set_option("conv3x3_rows4", rows4)
     cin, cout, H, W, coff = case
     x = torch.randn(1, cin + coff + 8, H, W)
     w = torch.randn(cout, cin, 3, 3) / (9 * cin) ** 0.5
@@ -495,7 +497,10 @@ def test_conv3x3_persistent_kernel(case, emode):
         y2 = h.conv(cw, xa, out_dtype=h.BF16)
         y3 = h.conv(cw, xa, out_dtype=h.F32, act=h.ACT_LRELU, slope=0.1, res=rf)
         names.append(h.lib().dcvc_last_kernel().decode())
-        got = [back(y), back(y2), back(y3)]
+        y5 = h.conv(cw, xa, out_dtype=h.BF16, in_op=h.IN_LRELU, in_slope=0.1, act=h.ACT_LRELU, slope=0.01,
+                    res=r1, scale=sc)
+        names.append(h.lib().dcvc_last_kernel().decode())
+        got = [back(y), back(y2), back(y3), back(y5)]
         if shuf:
             y4 = h.conv(cw, xa, out_dtype=h.BF16, shuffle=True, res=r3, scale=sc4)
             names.append(h.lib().dcvc_last_kernel().decode())
@@ -504,7 +509,8 @@ def test_conv3x3_persistent_kernel(case, emode):
         outs.append(got)
     h.set_option("conv3x3_persistent", 1)
     h.set_option("conv3x3_resident", 1)
-    h.set_option("conv3x3_epilogue", 2)
+    h.set_option("conv3x3_epilogue", 0)
+    h.set_option("conv3x3_rows4", 1)
     k = len(names) // 2
     assert all(n.startswith("conv3p_kernel") for n in names[:k]), names
     if emode == 0:
@@ -517,7 +523,7 @@ def test_conv3x3_persistent_kernel(case, emode):
     assert rel_err(outs[0][1], ref) < 2e-2
     if shuf:
         ref4 = F.pixel_shuffle(ref, 2) * sc4.cpu().view(1, -1, 1, 1)
-        assert rel_err(outs[0][3] - back(r3) * sc4.cpu().view(1, -1, 1, 1), ref4) < 2e-2
+        assert rel_err(outs[0][4] - back(r3) * sc4.cpu().view(1, -1, 1, 1), ref4) < 2e-2
 
 
 DCB_SHAPES = [(48, 32, False), (32, 64, False), (64, 128, False), (128, 128, False), (128, 64, False),
