@@ -11,10 +11,14 @@
 // This kernel is organised around hiding that latency instead:
 //   * one 512-thread workgroup per CU (grid = #CUs x n-blocks) keeps its
 //     BN-channel weight slice resident in LDS for the whole launch and walks
-//     16x16 output tiles (8 waves x 2 pixel rows);
+//     output tiles 16 pixels wide and 32, 16 or 8 rows high (8 waves x 4, 2
+//     or 1 pixel rows: the tallest whose weights, halo images and fp32
+//     epilogue tile fit the LDS; 32-row tiles read 7 LDS operands per 12
+//     MFMAs instead of 5 per 6 and 34 / 32 halo rows instead of 18 / 16);
 //   * the next tile's input is loaded into registers right after the current
 //     tile's image is published, so its HBM latency hides behind the current
-//     tile's MFMAs and epilogue (software pipeline, prefetch distance 1);
+//     tile's MFMAs and epilogue (software pipeline, prefetch distance 1; 2
+//     for 16-row tiles, where the registers allow a second set);
 //   * a thread's staging pieces run along the channel axis first, so the
 //     threads of a wave read whole contiguous pixel rows (CIN * 2 bytes per
 //     pixel) instead of 64-byte pieces one pixel stride apart;
