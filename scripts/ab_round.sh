@@ -4,8 +4,9 @@ set -u
 cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
 run() { local name=$1; shift; timeout -k 10 300 "$@" > gpurun_out/ab_$name.log 2>&1; local rc=$?; echo "$name rc=$rc"; case $rc in 0|1) ;; *) exit $rc ;; esac; }
-S=48x48@1088x1920r,48x48@1088x1920,96x48@1088x1920,80x48@1088x1920,32x32@1088x1920
-run c3_def python scripts/conv3_bench.py --reps 30 --shapes $S
-run c3_r4 python scripts/conv3_bench.py --reps 30 --shapes $S --opt conv3x3_rows4=1
-run c3_def2 python scripts/conv3_bench.py --reps 30 --shapes $S
-run c3_r4b python scripts/conv3_bench.py --reps 30 --shapes $S --opt conv3x3_rows4=1
+run gtest python -u -m pytest tests/test_gpu_kernels.py -m gpu -x -q -k "gemm" --timeout 120 --timeout-method thread -p no:cacheprovider
+run g_u1 python scripts/gemm_f32_bench.py --reps 50 --cfgs 0 --opt gemm1x1_f32_upfront=1
+run g_u0 python scripts/gemm_f32_bench.py --reps 50 --cfgs 0 --opt gemm1x1_f32_upfront=0 --opt gemm1x1_f32_direct=0
+run g_u1b python scripts/gemm_f32_bench.py --reps 50 --cfgs 0 --opt gemm1x1_f32_upfront=1
+run g_k3u1 python scripts/gemm_f32_bench.py --reps 50 --cfgs 0 --k3 --opt gemm1x1_f32_upfront=1
+run g_k3u0 python scripts/gemm_f32_bench.py --reps 50 --cfgs 0 --k3 --opt gemm1x1_f32_upfront=0 --opt gemm1x1_f32_direct=0
