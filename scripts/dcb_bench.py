@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--reps", type=int, default=30)
     ap.add_argument("--shapes", default="128x128@272x480,128x64@544x960,64x128@272x480,64x48@1088x1920")
     ap.add_argument("--kernels", default="stream,tile")
+    ap.add_argument("--opt", action="append", default=[], help="NAME=VALUE for dcvc_set_option (repeatable)")
     a = ap.parse_args()
     import torch
     from dcvc_amd import hip as K
@@ -28,6 +29,9 @@ def main():
     from dcvc_amd.weights import synthetic_state_dict
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
+    for o in a.opt:
+        name, val = o.split("=")
+        K.set_option(name, int(val))
     opts = {"stream": (1, 0), "persistent": (0, 1), "tile": (0, 0)}
     for sh in a.shapes.split(","):
         ch, hw = sh.split("@")
