@@ -28,10 +28,33 @@ import numpy as np
 import torch
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-PEAK_BF16_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
+PEAK_BF16_TFLOPS = 2500.0   # MI355X dense bf16 / f16 MFMA (MI355X_MICROARCH.md)
 PEAK_F32_TFLOPS = 157.3
+# split-fp16 convs (sconv.hip) issue 3 f16 MFMAs per fp32 product: their
+# algorithmic (fp32) flops are priced against a third of the f16 peak
+PEAK_F16X3_TFLOPS = PEAK_BF16_TFLOPS / 3
 PEAK_HBM_GBS = 8000.0
-BASELINE_METRIC = "encode+decode fps @1080p per GPU; bpp bit-exact + PSNR \u0394<1e-4 dB vs ref"
+# precisions held to the strict parity bar (tests/parity.py) carry the metric
+# with its qualifier; the bf16 modes are labelled as not held to it
+STRICT_PRECISIONS = ("split", "parity")
+
+
+def metric_name(args):
+    res = f"{args.width}x{args.height}"
+    if args.precision in STRICT_PRECISIONS:
+        return f"encode+decode fps @{res} per GPU; bpp bit-exact + PSNR \u0394<1e-4 dB vs ref"
+    return (f"encode+decode fps @{res} per GPU; {args.precision} precision, NOT held to the bit-exact bar "
+            "(see parity_check)")
+
+
+def peak_of(family, key):
+    """MFMA peak of one launch's compute type: f16x3 (split) convs, fp32
+    (f32 MFMA) convs and GEMMs, everything else bf16."""
+    if family == "sconv_kernel" or " f16x3 " in key:
+        return PEAK_F16X3_TFLOPS
+    if family.startswith("gemm1x1f") or " f32 " in key:
+        return PEAK_F32_TFLOPS
+    return PEAK_BF16_TFLOPS
 
 
 def parse():
@@ -49,9 +72,12 @@ def parse():
                     help="config C4: DCVC-DC YUV420 source coded as YCbCr 4:4:4 (dist_in_yuv420), 3840x2160")
     ap.add_argument("--gop", type=int, default=32)
     ap.add_argument("--q_index", type=int, default=0)
-    ap.add_argument("--precision", choices=["fast", "parity", "fast-bf16-tail"], default="fast",
-                    help="fast = bf16 feature convs + fp32 entropy-parameter tail (BASELINE C2); parity = fp32 "
-                         "end to end; fast-bf16-tail = bf16 MFMA for the entropy-parameter tail too (labelled)")
+    ap.add_argument("--precision", choices=["split", "parity", "fast", "fast-bf16-tail"], default="split",
+                    help="split = fp32 storage, every conv on split-fp16 MFMA (held to the strict parity bar, the "
+                         "default); parity = fp32 MFMA end to end; fast = bf16 feature convs + fp32 entropy tail "
+                         "and fast-bf16-tail = bf16 throughout (labelled lines, not held to the bar)")
+    ap.add_argument("--no-parity-check", action="store_true",
+                    help="skip the teacher-forced I + P parity check against the oracle (rank 0, N = 1)")
     ap.add_argument("--stream_part", type=int, default=8,
                     help="rANS stream parts (the reference's --stream_part_i/p); parts code in parallel threads")
     ap.add_argument("--lanes", type=int, default=3,
@@ -65,6 +91,7 @@ def parse():
                     help="only measure the oracle in the reference's worker-per-core mode with this many "
                          "single-thread workers (no GPU); prints the record profiles/cpu_baseline_workers.json holds")
     ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--launcher-selftest", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--profile-out", default="", help="per-shape kernel timing JSON of one P-frame")
     a = ap.parse_args()
     if a.yuv420 and a.model != "dc":
@@ -145,11 +172,13 @@ def host_info():
     return {"nproc": os.cpu_count() or 1, "usable": usable, "cpu": model}
 
 
-def oracle_ip_times(isd, psd, args, threads):
+def oracle_ip_times(isd, psd, args, threads, capture=None):
     """(t_I, t_P) seconds of the oracle (PyTorch fp32 CPU restatement, pinned
     to the reference) on one full-size I-frame and one full-size P-frame
     (1088x1920 for C3), each compress + rANS encode + rANS decode +
-    decompress in write mode, on `threads` torch threads."""
+    decompress in write mode, on `threads` torch threads.  capture (a dict)
+    receives what the parity check needs: per frame the padded input, the
+    coder calls, the rounding taps, the stream bits and the reconstruction."""
     from oracle import dc_oracle as O
     from oracle import rans_oracle as R
     from dcvc_amd.synth import moving_pattern, moving_pattern_yuv420, to_float
@@ -161,11 +190,14 @@ def oracle_ip_times(isd, psd, args, threads):
     tabs = {"i_y": (inet.y_cdf, inet.y_sizes, inet.y_offsets), "i_z": inet.z_tab,
             "p_y": (pnet.y_cdf, pnet.y_sizes, pnet.y_offsets), "p_z": pnet.z_tab, "p_mvz": pnet.mvz_tab}
 
+    nbytes = []
+
     def code(calls, pre):
         cc = [(s.clamp(-30000, 30000).to(torch.int16).numpy(), i.to(torch.int16).numpy(), tabs[pre + k])
               for k, s, i in calls]
         enc = R.DCStream()
         st = enc.encode(cc)
+        nbytes.append(len(st))
         dec = enc.decode(st)
         pos = [0]
 
@@ -185,20 +217,25 @@ def oracle_ip_times(isd, psd, args, threads):
         return torch.nn.functional.pad(x, (0, Wp - w, 0, Hp - h), mode="replicate")
 
     frames = [frame(t) for t in range(2)]
+    taps = [{}, {}] if capture is not None else [None, None]
     with torch.no_grad():
         t0 = time.time()
-        dec = code(inet.compress(frames[0], False, args.q_index), "i_")
-        xh = inet.decompress(dec, h, w, False, args.q_index)
+        calls_i = inet.compress(frames[0], False, args.q_index, tap=taps[0])
+        xh = inet.decompress(code(calls_i, "i_"), h, w, False, args.q_index)
         t_i = time.time() - t0
         dpb = {"ref_frame": xh, "ref_feature": None, "ref_mv_feature": None, "ref_y": None, "ref_mv_y": None}
         t0 = time.time()
-        dec = code(pnet.compress(frames[1], dpb, False, args.q_index, 1), "p_")
-        pnet.decompress(dpb, dec, h, w, False, args.q_index, 1)
+        calls_p = pnet.compress(frames[1], dpb, False, args.q_index, 1, tap=taps[1])
+        dpb_p = pnet.decompress(dpb, code(calls_p, "p_"), h, w, False, args.q_index, 1)
         t_p = time.time() - t0
+    if capture is not None:
+        capture.update(frames=frames, calls=[calls_i, calls_p], taps=taps,
+                       bits=[(nbytes[0] + 13) * 8, (nbytes[1] + 6) * 8], dpb_i=dpb,
+                       recon=[xh, dpb_p["ref_frame"] if isinstance(dpb_p, dict) else dpb_p], h=h, w=w)
     return t_i, t_p
 
 
-def cpu_baseline(isd, psd, args):
+def cpu_baseline(isd, psd, args, capture=None):
     """The oracle timed on this host in one process on `threads` cores: one
     full-size I-frame and one full-size P-frame; fps = the GOP average
     gop / (t_I + (gop - 1) t_P).  No area scaling.  The reference's own
@@ -208,7 +245,7 @@ def cpu_baseline(isd, psd, args):
     threads = max(1, min(args.cpu_threads, info["usable"]))
     h, w = args.height, args.width
     Hp, Wp = (h + 15) // 16 * 16, (w + 15) // 16 * 16
-    t_i, t_p = oracle_ip_times(isd, psd, args, threads)
+    t_i, t_p = oracle_ip_times(isd, psd, args, threads, capture)
     gop = args.gop
     fps = gop / (t_i + (gop - 1) * t_p)
     return {"value": fps, "unit": "frames/s", "cores": threads, "kind": "port",
@@ -264,6 +301,82 @@ def cpu_baseline_workers(args):
                      f"nproc {info['nproc']}, usable {info['usable']}, CPU {info['cpu']}",
            "ms_I": [round(t[0] * 1e3, 1) for t in times], "ms_P": [round(t[1] * 1e3, 1) for t in times]}
     print(json.dumps(rec), flush=True)
+
+
+def parity_check(cap, inet, pnet, args):
+    """The bench precision's own parity on the cpu_baseline frames: the
+    product codes the oracle's I-frame input and then the P-frame from the
+    ORACLE's decoded picture buffer (teacher forcing, as the strict tests do),
+    and every coder call is compared with the oracle's under tests/parity.py's
+    bar.  Reports differing symbols / indexes, bits and PSNR deltas."""
+    import tempfile
+    from tests.parity import compare_frame
+
+    def psnr(a, x):
+        mse = torch.mean((a.float().cpu()[..., :cap["h"], :cap["w"]].clamp(0, 1) - x[..., :cap["h"], :cap["w"]]) ** 2)
+        return float(-10 * torch.log10(mse))
+    out = []
+    with tempfile.TemporaryDirectory() as td:
+        for t in range(2):
+            xp = cap["frames"][t]
+            net = inet if t == 0 else pnet
+            net.entropy_coder.trace = []
+            path = os.path.join(td, f"{t}.bin")
+            if t == 0:
+                r = inet.encode_decode(xp.cuda(), False, args.q_index, path, pic_width=cap["w"], pic_height=cap["h"])
+                rec = r["x_hat"]
+            else:
+                dpb = {k: (v.cuda() if v is not None else None) for k, v in cap["dpb_i"].items()}
+                r = pnet.encode_decode(xp.cuda(), dpb, False, args.q_index, path, pic_width=cap["w"],
+                                       pic_height=cap["h"], frame_idx=1)
+                rec = r["dpb"]["ref_frame"]
+            torch.cuda.synchronize()
+            tr = net.entropy_coder.trace
+            net.entropy_coder.trace = None
+            enc = [(sy, ix) for k, sy, ix in tr if k == "enc"]
+            st = compare_frame(enc, cap["calls"][t], cap["taps"][t])
+            ff = st["first_flip"]
+            out.append({"frame": "IP"[t], "symbols": st["symbols"], "sym_diff": st["sym_diff"],
+                        "idx_diff": st["idx_diff"], "unexplained": len(st["unexplained"]),
+                        "first_flip_tie_dist": max(ff["tie_dist"]) if ff else None,
+                        "bits": int(r["bit"]), "bits_oracle": int(cap["bits"][t]),
+                        "dpsnr_db": psnr(rec, xp) - psnr(cap["recon"][t], xp)})
+    return {"teacher_forced": out, "bar": "tests/parity.py: every differing symbol / index a rounding tie "
+            "(< 2e-3 from the discontinuity), identical calls give identical bits and dPSNR < 1e-4 dB"}
+
+
+def launch_ranks(args):
+    """`bench.py --gpus N` outside a launcher: start N ranks of this script
+    under torch.distributed.run on 127.0.0.1, one per GPU (the reference fans
+    its jobs out to one worker per GPU, DCVC-DC/test_video.py:282-290), and
+    return their exit code.  Runs before anything touches the GPU."""
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd, env=env)
+
+
+def launcher_selftest(args):
+    """--launcher-selftest: the rank plumbing of the N-GPU bench without a GPU
+    (gloo): every rank joins, contributes its rank, and rank 0 prints one JSON
+    line with the world size it saw (tests/test_bench_launcher.py)."""
+    import torch.distributed as dist
+    dist.init_process_group("gloo")
+    world, rank = dist.get_world_size(), dist.get_rank()
+    t = torch.tensor([1.0, float(rank)])
+    dist.all_reduce(t)
+    dist.barrier()
+    elapsed = max_over_ranks(dist, 0.001 * (rank + 1), "cpu")
+    if rank == 0:
+        print(json.dumps({"n_gpus": world, "ranks_joined": int(t[0]), "rank_sum": int(t[1]),
+                          "max_elapsed": elapsed, "requested": args.gpus}), flush=True)
+    dist.destroy_process_group()
 
 
 def hem_q(sd_i, sd_p, rate):
@@ -325,53 +438,6 @@ def cpu_baseline_hem(isd, psd, args):
             **({"workers": _workers_record(args)} if _workers_record(args) else {})}
 
 
-WORKERS_RECORD = os.path.join(HERE, "profiles", "cpu_baseline_workers.json")
-
-
-def _workers_record(args):
-    """The committed worker-per-core measurement of this workload, if any."""
-    try:
-        with open(WORKERS_RECORD) as f:
-            rec = json.load(f)
-    except (OSError, ValueError):
-        return None
-    return rec if rec.get("workload") == [args.model, args.height, args.width, bool(args.yuv420)] else None
-
-
-def _worker(job):
-    isd, psd, args = job
-    return oracle_ip_times(isd, psd, args, 1)
-
-
-def cpu_baseline_workers(args):
-    """The reference's own CPU deployment, DCVC-DC/test_video.py:276-290: a
-    pool of `workers` processes with torch.set_num_threads(1) each, every
-    worker coding its own sequence; here each worker codes one full-size
-    I-frame and one full-size P-frame.  fps = workers x gop / (t_I + (gop - 1)
-    t_P) with each worker's own times (mean), i.e. all workers' frames over
-    the wall time of a GOP.  Runs without touching the GPU (a separate
-    invocation: ``python bench.py --cpu-baseline-workers N``)."""
-    import multiprocessing as mp
-    info = host_info()
-    n = args.cpu_baseline_workers
-    isd, psd = make_weights(None, 0, torch.device("cpu"), args.model)
-    t0 = time.time()
-    with mp.get_context("spawn").Pool(n) as pool:
-        times = pool.map(_worker, [(isd, psd, args)] * n)
-    wall = time.time() - t0
-    t_i = float(np.mean([t[0] for t in times]))
-    t_p = float(np.mean([t[1] for t in times]))
-    fps = n * args.gop / (t_i + (args.gop - 1) * t_p)
-    rec = {"value": fps, "unit": "frames/s", "cores": n, "kind": "port",
-           "workload": [args.model, args.height, args.width, bool(args.yuv420)],
-           "sample": f"{n} worker processes x 1 torch thread (DCVC-DC/test_video.py:276-290), each coding one "
-                     f"full-size I-frame (mean {t_i:.1f} s) and one full-size P-frame (mean {t_p:.1f} s) in write "
-                     f"mode; fps = workers x GOP {args.gop} / (t_I + {args.gop - 1} t_P); wall {wall:.0f} s; host "
-                     f"nproc {info['nproc']}, usable {info['usable']}, CPU {info['cpu']}",
-           "ms_I": [round(t[0] * 1e3, 1) for t in times], "ms_P": [round(t[1] * 1e3, 1) for t in times]}
-    print(json.dumps(rec), flush=True)
-
-
 def workload_key(argv):
     """(model, yuv420, height, width) of a bench.py command line."""
     toks = argv.split() if isinstance(argv, str) else list(argv)
@@ -422,6 +488,10 @@ def heartbeat(period=60.0):
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args))
+    if args.launcher_selftest:
+        return launcher_selftest(args)
     heartbeat()
     if args.cpu_baseline_workers:
         return cpu_baseline_workers(args)
@@ -446,7 +516,7 @@ def main():
         K.set_option(k, int(v))
     hem = args.model == "hem"
     isd, psd = make_weights(dist, rank, device, args.model)
-    prec = {"fast": Precision.fast(), "parity": Precision.parity(),
+    prec = {"split": Precision.split(), "fast": Precision.fast(), "parity": Precision.parity(),
             "fast-bf16-tail": Precision.fast(latent_compute=K.BF16)}[args.precision]
     if hem:
         from dcvc_amd.hem import DMC, IntraNoAR
@@ -605,7 +675,7 @@ def main():
                             "tflops": round(v[1] / max(v[0], 1e-12) / 1e12, 2),
                             "gbs": round(v[2] / max(v[0], 1e-12) / 1e9, 1)} for k, v in rows], f, indent=0)
         key, (tsec, fl, nb, n) = rows[0]
-        peak_f = PEAK_F32_TFLOPS if args.precision == "parity" else PEAK_BF16_TFLOPS
+        peak_f = peak_of(key.split("<")[0].split(" ")[0], key)
         t_mfma, t_hbm = fl / (peak_f * 1e12), nb / (PEAK_HBM_GBS * 1e9)
         if t_mfma >= t_hbm:
             ach = fl / tsec / 1e12
@@ -638,7 +708,8 @@ def main():
         roof["families_ms_per_P_frame"] = {k: round(v[0] * 1e3, 3) for k, v in fam.items()}
         # whole-frame layer roofline: sum over launches of max(F/P, B/BW)
         t_all = sum(v[0] for v in shapes.values())
-        t_roof = sum(max(v[1] / (peak_f * 1e12), v[2] / (PEAK_HBM_GBS * 1e9)) for v in shapes.values())
+        t_roof = sum(max(v[1] / (peak_of(k.split("<")[0].split(" ")[0], k) * 1e12), v[2] / (PEAK_HBM_GBS * 1e9))
+                     for k, v in shapes.items())
         roof["P_frame_kernels"] = {"gpu_ms": round(t_all * 1e3, 3), "roofline_ms": round(t_roof * 1e3, 3),
                                    "frac": round(t_roof / max(t_all, 1e-12), 4),
                                    "tflop": round(sum(v[1] for v in shapes.values()) / 1e12, 3),
@@ -650,9 +721,13 @@ def main():
         n_i = kinds.count("I")
         ti = [p for p, k in zip(per, kinds) if k == "I"]
         tp = [p for p, k in zip(per, kinds) if k == "P"]
-        cpu = None
+        cpu, parity = None, None
         if not args.no_cpu_baseline and world == 1:
-            cpu = cpu_baseline_hem(isd, psd, args) if hem else cpu_baseline(isd, psd, args)
+            cap = {} if (not hem and not args.yuv420 and not args.no_parity_check) else None
+            cpu = cpu_baseline_hem(isd, psd, args) if hem else cpu_baseline(isd, psd, args, cap)
+            if cap:
+                with torch.cuda.device(device), torch.cuda.stream(lanes[0].stream):
+                    parity = parity_check(cap, lanes[0].inet, lanes[0].pnet, args)
         timed_bits = [ln.bits[i] for ln in lanes for i in timed_idx]
         sse = np.concatenate([ln.stage.sums()[[ln.slot[i] for i in timed_idx]] for ln in lanes])
         if args.yuv420:
@@ -662,7 +737,7 @@ def main():
         else:
             psnr = {"psnr": round(float(np.mean([psnr_rgb(e, h, w) for e in sse])), 4)}
         line = {
-            "metric": BASELINE_METRIC,
+            "metric": metric_name(args),
             "value": round(world * args.lanes * args.steps / elapsed, 4),
             "unit": "frames/s",
             "n_gpus": world,
@@ -672,7 +747,8 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": {"fast": "bf16 features, fp32 entropy params", "parity": "f32",
+            "dtype": {"split": "f32 (convs on split-fp16 f16x3 MFMA, fp32 accumulation)", "parity": "f32",
+                      "fast": "bf16 features, fp32 entropy params",
                       "fast-bf16-tail": "bf16 (entropy-parameter tail in bf16 too)"}[args.precision],
             "data": "synthetic (moving sinusoid + noise frames, seeded random weights)",
             "config": {"workload": (f"C2 DCVC-HEM RGB {w}x{h} (zero pad {W}x{H}) IP={args.gop} write mode"
@@ -687,14 +763,18 @@ def main():
                        "ms_I": round(1e3 * float(np.mean(ti)), 2) if ti else None,
                        "ms_P": round(1e3 * float(np.mean(tp)), 2) if tp else None,
                        "timed_frames": [timed_idx[0], timed_idx[-1]],
-                       **({"fps_gop_avg": round(args.gop / (float(np.mean(ti)) + (args.gop - 1) * float(np.mean(tp))),
-                                                 3)} if ti and tp and args.lanes == 1 else {}),
+                       # steady-state GOP mix from the per-frame latencies: lanes x
+                       # gop / (t_I + (gop - 1) t_P), every lane count
+                       **({"fps_gop_avg": round(args.lanes * args.gop / (float(np.mean(ti))
+                                                                        + (args.gop - 1) * float(np.mean(tp))), 3)}
+                          if ti and tp else {}),
                        "step": f"one frame on each of {args.lanes} lane(s)",
                        "bpp": round(float(np.mean(timed_bits)) / (h * w), 5), **psnr,
                        **({"bits_per_lane": [int(sum(ln.bits[i] for i in timed_idx)) for ln in lanes]}
                           if args.lanes > 1 else {})},
             "roofline": roof,
             "cpu_baseline": cpu,
+            "parity_check": parity,
         }
         print(json.dumps(line), flush=True)
     import shutil

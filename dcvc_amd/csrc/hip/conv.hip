@@ -19,6 +19,7 @@
 #include "common.h"
 #include "epilogue.h"
 
+#include <cmath>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -488,9 +489,88 @@ bool valid_view(const dcvc_tensor &t) {
 
 }  // namespace
 
+// host f32 -> f16, round to nearest even (subnormals kept; |v| < 65520 assumed)
+static uint16_t host_f2h(float v) {
+  uint32_t u;
+  std::memcpy(&u, &v, 4);
+  const uint32_t sign = (u >> 16) & 0x8000u;
+  const int e = (int)((u >> 23) & 0xff) - 127;
+  uint32_t m = u & 0x7fffffu;
+  if (e > 15) return (uint16_t)(sign | 0x7c00u);          // overflow: infinity
+  if (e >= -14) {                                         // normal f16
+    uint32_t h = ((uint32_t)(e + 15) << 10) | (m >> 13);
+    const uint32_t rest = m & 0x1fffu;
+    if (rest > 0x1000u || (rest == 0x1000u && (h & 1u))) ++h;  // may carry into the exponent: still correct
+    return (uint16_t)(sign | h);
+  }
+  if (e < -25) return (uint16_t)sign;                     // below half the smallest subnormal
+  m |= 0x800000u;                                         // subnormal f16: value = m * 2^(e - 23)
+  const int shift = -e - 1;                               // 14..24: keep m >> shift as units of 2^-24
+  uint32_t h = m >> shift;
+  const uint32_t rest = m & ((1u << shift) - 1u), half = 1u << (shift - 1);
+  if (rest > half || (rest == half && (h & 1u))) ++h;
+  return (uint16_t)(sign | h);
+}
+static float host_h2f(uint16_t h) {
+  const uint32_t sign = (uint32_t)(h & 0x8000u) << 16;
+  const int e = (h >> 10) & 0x1f;
+  const uint32_t m = h & 0x3ffu;
+  float f;
+  if (e == 0) {
+    f = std::ldexp((float)m, -24);
+  } else {
+    uint32_t u = ((uint32_t)(e - 15 + 127) << 23) | (m << 13);
+    std::memcpy(&f, &u, 4);
+  }
+  uint32_t u;
+  std::memcpy(&u, &f, 4);
+  u |= sign;
+  std::memcpy(&f, &u, 4);
+  return f;
+}
+
+// DCVC_F16X3 layout (sconv.hip): per 32-channel input chunk c, a hi block
+// [rows][cout][32] then a lo block of the same shape, chunk c at c * 2 * kt *
+// cout * 32 halves.  A chunk with vc <= 16 (<= 8) valid channels packs tpk =
+// 2 (4) taps per 32-deep row: k = s * 8 + e holds tap tpk * row + s / (4 /
+// tpk), channel 32 c + (s % (4 / tpk)) * 8 + e.  hi = f16(w), lo = f16((w -
+// hi) * 2^11): w = hi + 2^-11 lo to ~2^-22.
+static int64_t pack_f16x3(const float *w, int cout, int cin, int kh, int kw, uint16_t *out) {
+  const int kt = kh * kw;
+  const int nch = (cin + 31) / 32;
+  const int vcl = cin - 32 * (nch - 1);
+  const int tpkl = vcl <= 8 ? 4 : vcl <= 16 ? 2 : 1;
+  const int64_t full = (int64_t)2 * kt * cout * 32;
+  const int64_t total = (int64_t)(nch - 1) * full + (int64_t)2 * ((kt + tpkl - 1) / tpkl) * cout * 32;
+  if (!out) return total;
+  for (int c = 0; c < nch; ++c) {
+    const int tpk = c == nch - 1 ? tpkl : 1;
+    const int spt = 4 / tpk;
+    const int rows = (kt + tpk - 1) / tpk;
+    uint16_t *hi = out + (int64_t)c * full;
+    uint16_t *lo = hi + (int64_t)rows * cout * 32;
+    for (int r = 0; r < rows; ++r)
+      for (int n = 0; n < cout; ++n)
+        for (int k = 0; k < 32; ++k) {
+          const int s = k >> 3, e = k & 7;
+          const int tap = tpk * r + s / spt;
+          const int ch = c * 32 + (s % spt) * 8 + e;
+          float v = 0.f;
+          if (tap < kt && ch < cin) v = w[(((int64_t)n * cin + ch) * kh + tap / kw) * kw + tap % kw];
+          const uint16_t h = host_f2h(v);
+          const int64_t o = ((int64_t)r * cout + n) * 32 + k;
+          hi[o] = h;
+          lo[o] = host_f2h((v - host_h2f(h)) * 2048.f);
+        }
+  }
+  return total;
+}
+
 extern "C" int64_t dcvc_conv_pack_weights(const float *w, int cout, int cin, int kh, int kw,
                                           int compute, void *out) {
-  if (!w || !out || cout <= 0 || cin <= 0 || kh <= 0 || kw <= 0) return DCVC_HIP_EINVAL;
+  if (!w || cout <= 0 || cin <= 0 || kh <= 0 || kw <= 0) return DCVC_HIP_EINVAL;
+  if (compute == DCVC_F16X3) return pack_f16x3(w, cout, cin, kh, kw, reinterpret_cast<uint16_t *>(out));
+  if (!out) return DCVC_HIP_EINVAL;
   const int cinp = (cin + kChunk - 1) / kChunk * kChunk;
   const int64_t total = (int64_t)cout * kh * kw * cinp;
   for (int n = 0; n < cout; ++n)
@@ -536,6 +616,10 @@ extern "C" void dcvc_internal_conv3p_occupancy(int v);
 extern "C" void dcvc_internal_conv3p_mode(int v);
 extern "C" void dcvc_internal_conv3p_rows4(int v);
 extern "C" void dcvc_internal_gemm1x1_bm(int v);
+extern "C" int dcvc_internal_sconv(const dcvc_conv_args *a, void *stream);
+extern "C" void dcvc_internal_sconv_occupancy(int v);
+extern "C" void dcvc_internal_sconv_waves(int v);
+extern "C" void dcvc_internal_sconv_resident(int v);
 
 extern "C" int dcvc_conv2d(const dcvc_conv_args *a, void *stream) {
   if (!a || !a->w || !valid_view(a->x) || !valid_view(a->y)) return DCVC_HIP_EINVAL;
@@ -588,6 +672,8 @@ extern "C" int dcvc_conv2d(const dcvc_conv_args *a, void *stream) {
     p.r2cs = a->res2.cstride;
     p.r2co = a->res2.coff;
   }
+  if (a->compute == DCVC_F16X3) return dcvc_internal_sconv(a, stream);   // the split-fp16 kernels only
+  if (a->compute != DCVC_F32 && a->compute != DCVC_BF16) return DCVC_HIP_EINVAL;
   if (a->kh == 3 && a->kw == 3 && a->stride == 1 && a->compute == DCVC_BF16 && g_use_conv3) {
     const int r = dcvc_internal_conv3x3(a, stream);
     if (r != DCVC_HIP_EUNSUPPORTED) return r;
@@ -708,6 +794,18 @@ extern "C" int dcvc_set_option(const char *name, int value) {
   }
   if (std::strcmp(name, "conv3x3_epilogue") == 0) {
     dcvc_internal_conv3p_mode(value);
+    return DCVC_HIP_OK;
+  }
+  if (std::strcmp(name, "sconv_resident") == 0) {
+    dcvc_internal_sconv_resident(value);
+    return DCVC_HIP_OK;
+  }
+  if (std::strcmp(name, "sconv_waves") == 0) {
+    dcvc_internal_sconv_waves(value);
+    return DCVC_HIP_OK;
+  }
+  if (std::strcmp(name, "sconv_occupancy") == 0) {
+    dcvc_internal_sconv_occupancy(value);
     return DCVC_HIP_OK;
   }
   if (std::strcmp(name, "conv3x3_rows4") == 0) {

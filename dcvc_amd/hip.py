@@ -15,10 +15,12 @@ import torch
 from ._native import hip_lib, check
 
 F32, BF16 = 0, 1
+F16X3 = 2   # conv compute only: split-fp16 operands, fp32 views (dcvc_hip.h DCVC_F16X3)
 ACT_NONE, ACT_LRELU, ACT_CLAMP01, ACT_ROUND = 0, 1, 2, 3
 IN_NONE, IN_LRELU, IN_GATE = 0, 1, 2
 
 _TORCH = {F32: torch.float32, BF16: torch.bfloat16}
+_CNAME = {F32: "f32", BF16: "bf16", F16X3: "f16x3"}
 _CODE = {torch.float32: F32, torch.bfloat16: BF16}
 
 
@@ -324,9 +326,13 @@ class ConvW:
         self.pad = (self.kh - 1) // 2
         self.compute = compute
         cinp = (self.cin + 31) // 32 * 32
-        n = self.cout * self.kh * self.kw * cinp
-        host = np.zeros(n, dtype=np.float32 if compute == F32 else np.uint16)
         wn = w.numpy()
+        if compute == F16X3:
+            n = int(check(int(lib().dcvc_conv_pack_weights(wn.ctypes.data_as(ctypes.c_void_p), self.cout, self.cin,
+                                                           self.kh, self.kw, compute, None)), "conv_pack_weights"))
+        else:
+            n = self.cout * self.kh * self.kw * cinp
+        host = np.zeros(n, dtype=np.float32 if compute == F32 else np.uint16)
         got = lib().dcvc_conv_pack_weights(wn.ctypes.data_as(ctypes.c_void_p), self.cout, self.cin,
                                            self.kh, self.kw, compute, host.ctypes.data_as(ctypes.c_void_p))
         check(int(got), "conv_pack_weights")
@@ -370,7 +376,7 @@ def conv(cw, x, y=None, *, out_dtype=None, in_op=IN_NONE, in_slope=0.0, act=ACT_
               + y.H * y.W * y.C * _esz(y.dtype) * (1 + (res is not None) + (res2 is not None)))
         kname = lib().dcvc_last_kernel().decode()
         _t1(e0, kname.split("<")[0], flops, nb, f"{kname} | k{cw.kh}s{cw.stride} {cw.cin}->{cw.cout} {x.H}x{x.W} "
-            f"{'bf16' if cw.compute == BF16 else 'f32'} in{x.dtype}out{y.dtype}{' shuf' if shuffle else ''}")
+            f"{_CNAME[cw.compute]} in{x.dtype}out{y.dtype}{' shuf' if shuffle else ''}")
     return y
 
 

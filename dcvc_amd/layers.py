@@ -9,14 +9,18 @@ channel windows of one NHWC buffer (``Act.ch``).
 Precision policy (``Precision``): feature-domain activations (full to 1/8
 resolution) are stored in ``feat`` and convolved with ``feat_compute``;
 latent-domain tensors (1/16 and 1/64: y, z, priors, entropy parameters) are
-stored fp32 and convolved with ``latent_compute``.  ``Precision.parity()`` is
-fp32 everywhere (f32 MFMA, exact fp32 fma chains); ``Precision.fast()`` is
-bf16 MFMA with fp32 accumulation and fp32 latents.
+stored fp32 and convolved with ``latent_compute``.
+  * ``Precision.split()`` (the bench default): fp32 storage everywhere, every
+    dense conv on split-fp16 operands (x = hi + 2^-11 lo, three f16 MFMAs per
+    product, fp32 accumulation; sconv.hip): held to the strict parity bar.
+  * ``Precision.parity()``: fp32 everywhere on f32 MFMA (exact fp32 fma chains).
+  * ``Precision.fast()``: bf16 feature maps and bf16 MFMA, fp32 latents; not
+    held to the strict bar (labelled lines only).
 """
 import torch
 
 from . import hip as K
-from .hip import Act, F32, BF16, ACT_LRELU, ACT_NONE, IN_LRELU, IN_GATE
+from .hip import Act, F32, BF16, F16X3, ACT_LRELU, ACT_NONE, IN_LRELU, IN_GATE
 
 
 FUSE_DCB = True   # fused DepthConvBlock kernel where instantiated (A/B switch)
@@ -36,6 +40,18 @@ class Precision:
     @staticmethod
     def fast(latent_compute=F32):
         return Precision(BF16, BF16, latent_compute)
+
+    @staticmethod
+    def split():
+        return Precision(F32, F16X3, F16X3)
+
+    @property
+    def name(self):
+        if self.feat_compute == F16X3:
+            return "split"
+        if self.feat == F32:
+            return "parity"
+        return "fast" if self.latent_compute == F32 else "fast-bf16-tail"
 
 
 class Ctx:
@@ -98,8 +114,8 @@ class Ctx:
         return self.prec.latent if latent else self.prec.feat
 
     def fit(self, x, compute):
-        """f32 compute needs f32 inputs; cast a view when a layer crosses domains."""
-        if compute == F32 and x.dtype != F32:
+        """f32 / f16x3 compute needs f32 inputs; cast a view when a layer crosses domains."""
+        if compute != BF16 and x.dtype != F32:
             return cast(x, F32)
         return x
 

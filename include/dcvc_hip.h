@@ -31,6 +31,11 @@ extern "C" {
 #define DCVC_HIP_EUNSUPPORTED (-3)
 
 enum dcvc_dtype { DCVC_F32 = 0, DCVC_BF16 = 1 };
+/* Conv compute type (dcvc_conv_args.compute) beside DCVC_F32 / DCVC_BF16:
+ * fp32 operands split into two fp16 values each (x = hi + 2^-11 lo) and
+ * multiplied as xh*wh + 2^-11 (xh*wl + xl*wh) on f16 MFMA with fp32
+ * accumulation (~2^-21 relative operand error); fp32 input and output views. */
+#define DCVC_F16X3 2
 
 enum dcvc_act {
   DCVC_ACT_NONE = 0,
@@ -72,7 +77,8 @@ typedef struct dcvc_conv_args {
   const float *bias;      /* [Cout] or NULL                                */
   int cin, cout;          /* conv channels (cout before pixel shuffle)    */
   int kh, kw, stride, pad;
-  int compute;            /* DCVC_BF16: bf16 MFMA, DCVC_F32: f32 MFMA      */
+  int compute;            /* DCVC_BF16: bf16 MFMA, DCVC_F32: f32 MFMA,
+                             DCVC_F16X3: split-fp16 MFMA (fp32 views)     */
   int in_op;              /* dcvc_in_op                                    */
   float in_slope;
   int act;                /* dcvc_act                                      */
@@ -86,7 +92,10 @@ typedef struct dcvc_conv_args {
 /* Pack reference-layout fp32 weights [Cout][Cin][kh][kw] (host pointer) into
  * the kernel layout [Cout][kh][kw][Cin_pad] (Cin_pad = Cin rounded up to 32)
  * in dtype `compute`, written to host buffer `out`.  Returns the number of
- * elements written (Cout*kh*kw*Cin_pad) or a negative code. */
+ * elements written (Cout*kh*kw*Cin_pad) or a negative code.
+ * compute = DCVC_F16X3 writes uint16 fp16 halves in the split layout of
+ * sconv.hip (per 32-channel chunk a hi and a lo block); out = NULL then
+ * returns the element count without writing. */
 int64_t dcvc_conv_pack_weights(const float *w, int cout, int cin, int kh,
                                int kw, int compute, void *out);
 int dcvc_conv2d(const dcvc_conv_args *a, void *stream);

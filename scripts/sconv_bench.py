@@ -1,0 +1,65 @@
+"""Time split-fp16 convolutions (sconv.hip) on the DC 1080p P-frame shapes.
+
+    python scripts/sconv_bench.py [--reps 20] [--shapes 48x48@1088x1920k3r,...] [--opt NAME=VALUE]
+
+A shape is CINxCOUT@HxW then kK (kernel size, default 3), sS (stride,
+default 1) and "r" for an fp32 residual input.  One JSON line per shape:
+kernel, us/launch, algorithmic GB/s (fp32 input, split weights, output,
+residual once each) and fp32-equivalent TFLOP/s (against 2500/3 = 833 peak).
+"""
+import argparse
+import json
+import os
+import re
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+DEFAULT = ("48x48@1088x1920k3r,64x64@544x960k3r,96x48@1088x1920k3,128x192@544x960k3,32x64@1088x1920k7,"
+           "64x32@1088x1920k7,48x192@1088x1920k1,192x48@1088x1920k1r,384x384@68x120k1,1024x384@68x120k1,"
+           "56x64@1088x1920k3s2")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--shapes", default=DEFAULT)
+    ap.add_argument("--opt", action="append", default=[], help="NAME=VALUE for dcvc_set_option (repeatable)")
+    a = ap.parse_args()
+    import torch
+    from dcvc_amd import hip as K
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(0)
+    for o in a.opt:
+        name, val = o.split("=")
+        K.set_option(name, int(val))
+    for sh in a.shapes.split(","):
+        m = re.fullmatch(r"(\d+)x(\d+)@(\d+)x(\d+)(?:k(\d))?(?:s(\d))?(r?)", sh)
+        cin, cout, H, W = (int(m.group(i)) for i in range(1, 5))
+        k = int(m.group(5) or 3)
+        s = int(m.group(6) or 1)
+        res = m.group(7) == "r"
+        cw = K.ConvW(torch.randn(cout, cin, k, k) / (cin * k * k) ** 0.5, torch.randn(cout) * 0.1, s, K.F16X3, dev)
+        x = K.from_nchw(torch.randn(1, cin, H, W, device=dev), K.F32)
+        Ho, Wo = cw.out_hw(H, W)
+        r = K.from_nchw(torch.randn(1, cout, Ho, Wo, device=dev), K.F32) if res else None
+        y = K.empty(Ho, Wo, cout, K.F32, dev)
+        for _ in range(3):
+            K.conv(cw, x, y, act=K.ACT_LRELU, slope=0.1, res=r)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(a.reps):
+            K.conv(cw, x, y, act=K.ACT_LRELU, slope=0.1, res=r)
+        e1.record()
+        torch.cuda.synchronize()
+        us = e0.elapsed_time(e1) * 1e3 / a.reps
+        nb = 4 * (H * W * cin + Ho * Wo * cout * (2 if res else 1)) + cw.w.numel() * 2
+        fl = 2.0 * Ho * Wo * cin * cout * k * k
+        print(json.dumps({"shape": sh, "opt": a.opt, "kernel": K.lib().dcvc_last_kernel().decode(), "us": round(us, 2),
+                          "gbs": round(nb / us / 1e3, 1), "tflops": round(fl / us / 1e6, 1),
+                          "frac_mfma": round(fl / us / 1e6 / 833.3, 3)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

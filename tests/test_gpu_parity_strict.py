@@ -44,7 +44,7 @@ def psnr(a, b):
 class Pair:
     """Oracle and product codecs built from the same state dicts."""
 
-    def __init__(self, i_sd, p_sd):
+    def __init__(self, i_sd, p_sd, prec="parity"):
         from oracle import dc_oracle as O
         from oracle import rans_oracle as R
         from dcvc_amd.dc import DMC, IntraNoAR
@@ -55,8 +55,9 @@ class Pair:
         self.tabs = {"i_y": (self.oi.y_cdf, self.oi.y_sizes, self.oi.y_offsets), "i_z": self.oi.z_tab,
                      "p_y": (self.op.y_cdf, self.op.y_sizes, self.op.y_offsets), "p_z": self.op.z_tab,
                      "p_mvz": self.op.mvz_tab}
-        self.pi = IntraNoAR(precision=Precision.parity()).load_state_dict(i_sd)
-        self.pp = DMC(precision=Precision.parity()).load_state_dict(p_sd)
+        P = getattr(Precision, prec)
+        self.pi = IntraNoAR(precision=P()).load_state_dict(i_sd)
+        self.pp = DMC(precision=P()).load_state_dict(p_sd)
         self.pi.update(force=True)
         self.pp.update(force=True)
 
@@ -118,17 +119,22 @@ def run_teacher_forced(pair, frames, q, h, w, name):
     return stats
 
 
+PRECS = ["split", "parity"]   # split = the bench's precision (split-fp16 MFMA), parity = fp32 MFMA
+
+
+@pytest.mark.parametrize("prec", PRECS)
 @pytest.mark.parametrize("tag", ["A", "B"])
-def test_strict_parity_golden(dc_golden, tag):
+def test_strict_parity_golden(dc_golden, tag, prec):
     meta = dc_golden.meta[tag]
-    pair = Pair(dc_golden.i_state_dict(), dc_golden.p_state_dict())
+    pair = Pair(dc_golden.i_state_dict(), dc_golden.p_state_dict(), prec)
     frames = [dc_golden.frame_tensor(tag, t) for t in range(meta["frames"])]
-    stats = run_teacher_forced(pair, frames, meta["q_index"], meta["h"], meta["w"], f"golden_{tag}")
+    stats = run_teacher_forced(pair, frames, meta["q_index"], meta["h"], meta["w"], f"golden_{tag}_{prec}")
     for st, msg in stats:
         print(msg)
 
 
-def test_strict_parity_c3_1080p():
+@pytest.mark.parametrize("prec", PRECS)
+def test_strict_parity_c3_1080p(prec):
     """Config C3 at full size: I-frame + P-frame (frame_idx 1), q_index 0."""
     import bench
     from dcvc_amd.synth import moving_pattern, to_float
@@ -138,21 +144,22 @@ def test_strict_parity_c3_1080p():
     for t in range(2):
         x = torch.from_numpy(to_float(moving_pattern(h, w, t, seed=1))).unsqueeze(0)
         frames.append((x, torch.nn.functional.pad(x, (0, 0, 0, 8), mode="replicate")))
-    pair = Pair(isd, psd)
-    stats = run_teacher_forced(pair, frames, 0, h, w, "C3_1080p")
+    pair = Pair(isd, psd, prec)
+    stats = run_teacher_forced(pair, frames, 0, h, w, f"C3_1080p_{prec}")
     for st, msg in stats:
         print(msg)
 
 
-def test_strict_parity_c3small_survey_recipe():
+@pytest.mark.parametrize("prec", PRECS)
+def test_strict_parity_c3small_survey_recipe(prec):
     """The survey's C3-small recipe (default-init weights, 4 torch.rand 256x256
     frames, q_index 0): strict parity against the oracle, and on every frame
     whose calls all agree, the survey's recorded bits exactly."""
     from tests.test_oracle_c3small import C3Small
     c3s = C3Small()
     frames = [(x, x) for x in c3s.frames()]
-    pair = Pair(c3s.i_sd, c3s.p_sd)
-    stats = run_teacher_forced(pair, frames, 0, 256, 256, "C3small_survey")
+    pair = Pair(c3s.i_sd, c3s.p_sd, prec)
+    stats = run_teacher_forced(pair, frames, 0, 256, 256, f"C3small_survey_{prec}")
     for (st, msg), want in zip(stats, c3s.meta["survey_bits"]):
         print(msg)
         if st["identical"]:
@@ -164,7 +171,7 @@ class HemPair(Pair):
     one headerless int32 stream per frame (the reference's
     BufferedRansEncoder), coded here by the oracle's C restatement."""
 
-    def __init__(self, i_sd, p_sd, q):
+    def __init__(self, i_sd, p_sd, q, prec="parity"):
         from oracle import hem_oracle as O
         from oracle import rans_oracle as R
         from dcvc_amd.hem import DMC, IntraNoAR
@@ -175,8 +182,9 @@ class HemPair(Pair):
         self.op = O.DMCOracle(p_sd, R.pmf_to_quantized_cdf)
         self.tabs = {"i_y": self.oi.tab_y[:3], "i_z": self.oi.tab_z[:3], "p_y": self.op.tab_y[:3],
                      "p_z": self.op.tab_z[:3], "p_mvz": self.op.tab_mvz[:3]}
-        self.pi = IntraNoAR(precision=Precision.parity()).load_state_dict(i_sd)
-        self.pp = DMC(precision=Precision.parity()).load_state_dict(p_sd)
+        P = getattr(Precision, prec)
+        self.pi = IntraNoAR(precision=P()).load_state_dict(i_sd)
+        self.pp = DMC(precision=P()).load_state_dict(p_sd)
         self.pi.update(force=True)
         self.pp.update(force=True)
 
@@ -242,16 +250,17 @@ class HemPair(Pair):
         return enc, r["bit"], rec.clamp(0, 1)
 
 
+@pytest.mark.parametrize("prec", PRECS)
 @pytest.mark.parametrize("tag", ["C1", "A", "B"])
-def test_strict_parity_hem(tag):
+def test_strict_parity_hem(tag, prec):
     """DCVC-HEM: config C1 (4 random 256x256 frames, IP=4; write mode codes
     I, P1, P2 as the survey's recipe) and the golden sequences A, B."""
     from tests.hem_fixtures import HEMGolden
     g = HEMGolden()
     meta = g.meta[tag]
-    pair = HemPair(g.i_state_dict(), g.p_state_dict(), g.q(tag))
+    pair = HemPair(g.i_state_dict(), g.p_state_dict(), g.q(tag), prec)
     frames = [g.frame_tensor(tag, t) for t in range(g.write_frames(tag))]
-    stats = run_teacher_forced(pair, frames, None, meta["h"], meta["w"], f"hem_{tag}")
+    stats = run_teacher_forced(pair, frames, None, meta["h"], meta["w"], f"hem_{tag}_{prec}")
     for st, msg in stats:
         print(msg)
 

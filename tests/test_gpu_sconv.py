@@ -1,0 +1,144 @@
+"""The split-fp16 conv kernels (sconv.hip, compute DCVC_F16X3) against fp64
+convolutions of the same fp32 operands on the CPU.
+
+The split keeps ~21 bits of every operand (x = hi + 2^-11 lo, the lo * lo
+product dropped), so the kernel must land within a few fp32 roundings of the
+exact result: the bound is 4e-6 of the output's magnitude, while dropping
+one product of a K = 432 sum moves it by ~1e-2 and bf16 operands by ~4e-3.
+Shapes cover every kernel size / stride / tap packing the codec uses: 32-
+channel chunks, 16- and 8-channel last chunks (2 and 4 taps per MFMA K step),
+channel counts below 8 (scalar staging), channel views, every epilogue op.
+"""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+TOL = 4e-6
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    torch.manual_seed(0)
+
+
+def K():
+    from dcvc_amd import hip
+    return hip
+
+
+def rel_err(got, ref):
+    scale = ref.abs().max().item() + 1e-12
+    return (got.double() - ref).abs().max().item() / scale
+
+
+CASES = [
+    # cin, cout, k, stride, H, W
+    (48, 48, 3, 1, 37, 53),
+    (64, 64, 3, 1, 70, 90),
+    (32, 64, 3, 1, 19, 40),
+    (96, 48, 3, 1, 21, 35),
+    (80, 48, 3, 1, 17, 33),
+    (128, 192, 3, 1, 11, 23),
+    (3, 48, 3, 1, 20, 33),
+    (6, 64, 3, 1, 16, 20),
+    (2, 64, 3, 2, 34, 40),
+    (51, 64, 3, 2, 34, 40),
+    (56, 64, 3, 2, 36, 46),
+    (64, 96, 3, 2, 18, 30),
+    (8, 32, 7, 1, 23, 29),
+    (16, 2, 7, 1, 16, 16),
+    (32, 64, 7, 1, 24, 37),
+    (64, 32, 7, 1, 20, 21),
+    (32, 16, 7, 1, 18, 33),
+    (384, 384, 1, 1, 9, 13),
+    (1024, 384, 1, 1, 5, 6),
+    (48, 192, 1, 1, 33, 47),
+    (192, 48, 1, 1, 33, 47),
+    (128, 64, 1, 2, 12, 10),
+    (2, 64, 1, 2, 30, 34),
+    (16, 16, 1, 1, 64, 80),
+]
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_sconv_matches_fp64(case):
+    h = K()
+    cin, cout, k, s, H, W = case
+    g = torch.Generator().manual_seed(cin * 1000 + cout + k)
+    x = torch.randn(1, cin, H, W, generator=g)
+    x[:, :, ::3] *= 1e-3          # small values: the lo parts go subnormal in fp16
+    w = torch.randn(cout, cin, k, k, generator=g) / (cin * k * k) ** 0.5
+    b = torch.randn(cout, generator=g) * 0.1
+    ref = F.conv2d(x.double(), w.double(), b.double(), stride=s, padding=(k - 1) // 2)
+    cw = h.ConvW(w, b, s, h.F16X3)
+    y = h.conv(cw, h.from_nchw(x, h.F32), out_dtype=h.F32)
+    torch.cuda.synchronize()
+    assert h.lib().dcvc_last_kernel().decode().startswith("sconv_kernel")
+    err = rel_err(y.nchw().cpu(), ref)
+    assert err < TOL, (case, err)
+
+
+def test_sconv_fused_epilogue_and_views():
+    """in_op lrelu, bias, act, residual, res2, scale on channel views; pixel
+    shuffle; the ConvFFN2 gate input op."""
+    h = K()
+    cin, cout, H, W = 64, 48, 29, 37
+    g = torch.Generator().manual_seed(7)
+    big = torch.randn(1, cin + 16, H, W, generator=g)
+    x = big[:, 8:8 + cin]
+    w = torch.randn(cout, cin, 3, 3, generator=g) / (cin * 9) ** 0.5
+    b = torch.randn(cout, generator=g) * 0.1
+    r = torch.randn(1, cout, H, W, generator=g)
+    r2 = torch.randn(1, cout, H, W, generator=g)
+    sc = torch.rand(cout, generator=g) + 0.5
+    xd = F.leaky_relu(x.double(), 0.2)
+    ref = (r2.double() + (r.double() + F.leaky_relu(F.conv2d(xd, w.double(), b.double(), padding=1), 0.1))) \
+        * sc.double().view(1, -1, 1, 1)
+    cw = h.ConvW(w, b, 1, h.F16X3)
+    xa = h.from_nchw(big, h.F32).ch(8, cin)
+    out = h.empty(H, W, cout + 8, h.F32)
+    ra = h.empty(H, W, cout + 4, h.F32)
+    h.copy(h.from_nchw(r, h.F32), ra.ch(4, cout))
+    r2a = h.from_nchw(r2, h.F32)
+    h.conv(cw, xa, out.ch(8, cout), in_op=h.IN_LRELU, in_slope=0.2, act=h.ACT_LRELU, slope=0.1,
+           res=ra.ch(4, cout), res2=r2a, scale=sc.cuda())
+    torch.cuda.synchronize()
+    assert rel_err(out.ch(8, cout).nchw().cpu(), ref) < TOL
+
+    # pixel shuffle (subpel_conv3x3: 96 -> 4 x 32)
+    cin, cout = 96, 128
+    x = torch.randn(1, cin, 15, 22, generator=g)
+    w = torch.randn(cout, cin, 3, 3, generator=g) / (cin * 9) ** 0.5
+    b = torch.randn(cout, generator=g) * 0.1
+    ref = F.pixel_shuffle(F.conv2d(x.double(), w.double(), b.double(), padding=1), 2)
+    y = h.conv(h.ConvW(w, b, 1, h.F16X3), h.from_nchw(x, h.F32), shuffle=True)
+    torch.cuda.synchronize()
+    assert rel_err(y.nchw().cpu(), ref) < TOL
+
+    # ConvFFN2 gate: conv_out(x1 * lrelu(x2, 0.1)) + residual
+    c = 64
+    x = torch.randn(1, 2 * c, 20, 36, generator=g)
+    w = torch.randn(c, c, 1, 1, generator=g) / c ** 0.5
+    b = torch.randn(c, generator=g) * 0.1
+    x1, x2 = x.double().chunk(2, 1)
+    ref = F.conv2d(x1 * F.leaky_relu(x2, 0.1), w.double(), b.double())
+    y = h.conv(h.ConvW(w, b, 1, h.F16X3), h.from_nchw(x, h.F32), in_op=h.IN_GATE, in_slope=0.1)
+    torch.cuda.synchronize()
+    assert rel_err(y.nchw().cpu(), ref) < TOL
+
+
+def test_sconv_fp16_subnormal_operands():
+    """Inputs around 1e-6 .. 1e-4 (fp16 subnormal hi parts): the kernel still
+    follows fp64 to the bound, relative to the output's magnitude."""
+    h = K()
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(1, 32, 16, 16, generator=g) * 1e-5
+    w = torch.randn(32, 32, 3, 3, generator=g) * 0.05
+    ref = F.conv2d(x.double(), w.double(), None, padding=1)
+    y = h.conv(h.ConvW(w, torch.zeros(32), 1, h.F16X3), h.from_nchw(x, h.F32), out_dtype=h.F32)
+    torch.cuda.synchronize()
+    assert rel_err(y.nchw().cpu(), ref) < 1e-4
