@@ -41,6 +41,18 @@ __device__ __forceinline__ void st(void *base, int64_t i, float v) {
   Elem<T>::store(reinterpret_cast<T *>(base) + i, v);
 }
 
+// Orders a wave's LDS writes before its later LDS reads of the same region by
+// other lanes of that wave (and reads before later overwrites) in the
+// wave-private phases of the fused kernels.  LDS operations of one wave
+// complete in order, so no wait or barrier instruction is needed; the fences
+// keep the compiler from moving a read above a write (or a write above a read)
+// whose same-lane addresses it can prove disjoint.
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // Epilogue / prologue activations (see dcvc_act in dcvc_hip.h).
 __device__ __forceinline__ float apply_act(int act, float v, float slope) {
   switch (act) {

@@ -18,6 +18,7 @@
 // them (see dcvc_conv_args in include/dcvc_hip.h).
 #include "common.h"
 #include "epilogue.h"
+#include "split.h"
 
 #include <cmath>
 #include <cstdarg>
@@ -489,46 +490,6 @@ bool valid_view(const dcvc_tensor &t) {
 
 }  // namespace
 
-// host f32 -> f16, round to nearest even (subnormals kept; |v| < 65520 assumed)
-static uint16_t host_f2h(float v) {
-  uint32_t u;
-  std::memcpy(&u, &v, 4);
-  const uint32_t sign = (u >> 16) & 0x8000u;
-  const int e = (int)((u >> 23) & 0xff) - 127;
-  uint32_t m = u & 0x7fffffu;
-  if (e > 15) return (uint16_t)(sign | 0x7c00u);          // overflow: infinity
-  if (e >= -14) {                                         // normal f16
-    uint32_t h = ((uint32_t)(e + 15) << 10) | (m >> 13);
-    const uint32_t rest = m & 0x1fffu;
-    if (rest > 0x1000u || (rest == 0x1000u && (h & 1u))) ++h;  // may carry into the exponent: still correct
-    return (uint16_t)(sign | h);
-  }
-  if (e < -25) return (uint16_t)sign;                     // below half the smallest subnormal
-  m |= 0x800000u;                                         // subnormal f16: value = m * 2^(e - 23)
-  const int shift = -e - 1;                               // 14..24: keep m >> shift as units of 2^-24
-  uint32_t h = m >> shift;
-  const uint32_t rest = m & ((1u << shift) - 1u), half = 1u << (shift - 1);
-  if (rest > half || (rest == half && (h & 1u))) ++h;
-  return (uint16_t)(sign | h);
-}
-static float host_h2f(uint16_t h) {
-  const uint32_t sign = (uint32_t)(h & 0x8000u) << 16;
-  const int e = (h >> 10) & 0x1f;
-  const uint32_t m = h & 0x3ffu;
-  float f;
-  if (e == 0) {
-    f = std::ldexp((float)m, -24);
-  } else {
-    uint32_t u = ((uint32_t)(e - 15 + 127) << 23) | (m << 13);
-    std::memcpy(&f, &u, 4);
-  }
-  uint32_t u;
-  std::memcpy(&u, &f, 4);
-  u |= sign;
-  std::memcpy(&f, &u, 4);
-  return f;
-}
-
 // DCVC_F16X3 layout (sconv.hip): per 32-channel input chunk c, a hi block
 // [rows][cout][32] then a lo block of the same shape, chunk c at c * 2 * kt *
 // cout * 32 halves.  A chunk with vc <= 16 (<= 8) valid channels packs tpk =
@@ -557,10 +518,8 @@ static int64_t pack_f16x3(const float *w, int cout, int cin, int kh, int kw, uin
           const int ch = c * 32 + (s % spt) * 8 + e;
           float v = 0.f;
           if (tap < kt && ch < cin) v = w[(((int64_t)n * cin + ch) * kh + tap / kw) * kw + tap % kw];
-          const uint16_t h = host_f2h(v);
           const int64_t o = ((int64_t)r * cout + n) * 32 + k;
-          hi[o] = h;
-          lo[o] = host_f2h((v - host_h2f(h)) * 2048.f);
+          host_split(v, hi[o], lo[o]);
         }
   }
   return total;
@@ -620,6 +579,7 @@ extern "C" int dcvc_internal_sconv(const dcvc_conv_args *a, void *stream);
 extern "C" void dcvc_internal_sconv_occupancy(int v);
 extern "C" void dcvc_internal_sconv_waves(int v);
 extern "C" void dcvc_internal_sconv_resident(int v);
+extern "C" void dcvc_internal_sconv_res_waves(int v);
 
 extern "C" int dcvc_conv2d(const dcvc_conv_args *a, void *stream) {
   if (!a || !a->w || !valid_view(a->x) || !valid_view(a->y)) return DCVC_HIP_EINVAL;
@@ -794,6 +754,10 @@ extern "C" int dcvc_set_option(const char *name, int value) {
   }
   if (std::strcmp(name, "conv3x3_epilogue") == 0) {
     dcvc_internal_conv3p_mode(value);
+    return DCVC_HIP_OK;
+  }
+  if (std::strcmp(name, "sconv_res_waves") == 0) {
+    dcvc_internal_sconv_res_waves(value);
     return DCVC_HIP_OK;
   }
   if (std::strcmp(name, "sconv_resident") == 0) {

@@ -366,7 +366,8 @@ __global__ void __launch_bounds__(NTHR) dcbp_kernel(DcbP p) {
     }
     // From here to P5 every wave touches only its own pixel tile's rows of
     // Cs, Ds / Hs and (read-only) Xs: a wave's LDS operations complete in
-    // order, so P3 -> P4 -> P5 need no barriers.
+    // order, so P3 -> P4 -> P5 need no barriers, only wave-scope ordering.
+    wave_lds_sync();
 
     // ---- P4: FFN over 64-channel hidden slices
     f32x4 acc[NPT][NTO];
@@ -382,6 +383,7 @@ __global__ void __launch_bounds__(NTHR) dcbp_kernel(DcbP p) {
 #pragma unroll
         for (int j = 0; j < NTH; ++j) hacc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
       mma<RLO, RLO, NPT, NTH>(hacc, Cs, rowi, Wl + G_::OF1 + s * 64 * RLO, COUT, lane);
+      wave_lds_sync();   // the previous slice's Hs reads before these writes
 #pragma unroll
       for (int i = 0; i < NPT; ++i)
 #pragma unroll
@@ -391,8 +393,10 @@ __global__ void __launch_bounds__(NTHR) dcbp_kernel(DcbP p) {
           for (int q = 0; q < 4; ++q) v[q] = lrelu(hacc[i][j][q] + bf1[s * 64 + j * 16 + hi * 4 + q], p.slope_ffn);
           put4<64>(Hs, rowi[i] + col, j * 16 + hi * 4, v);
         }
+      wave_lds_sync();   // Hs written before other lanes read it
       mma<64, 64, NPT, NTO>(acc, Hs, rowi, Wl + G_::OF2 + s * NTO * 16 * 64, 64, lane);
     }
+    wave_lds_sync();   // P4's Cs reads before P5 overwrites the rows
 
     // ---- P5: out = dc + lrelu(acc + bf2) [* scale] -> Cs (bf16), whole-line stores
 #pragma unroll

@@ -470,6 +470,7 @@ __global__ void __launch_bounds__(NTHR) dcbs_kernel(DcbP p) {
           zero(hacc);
 #pragma unroll
           for (int kc = 0; kc < KCO; ++kc) mma<COUT, 1, 4>(hacc, Cs, rowf, Bs + kc * 64 * 64, 0, lane_, kc * 64);
+          wave_lds_sync();   // the previous slice's Hs reads (other lanes) before these writes
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
             float v[4];
@@ -477,6 +478,7 @@ __global__ void __launch_bounds__(NTHR) dcbs_kernel(DcbP p) {
             for (int q = 0; q < 4; ++q) v[q] = lrelu(hacc[0][j][q] + el(f1v[j], q), p.slope_ffn);
             put4<64>(Hs, rowf[0] + col, j * 16 + hi * 4, v);
           }
+          wave_lds_sync();   // Hs written before other lanes read it
           mma<64, 1, NTO>(acc, Hs, rowf, Bs + KCO * 64 * 64, 0, lane_, 0);
         }
       }

@@ -44,15 +44,11 @@
 //     order and stores fp32 whole lines per wave instruction.
 #include "common.h"
 #include "epilogue.h"
+#include "split.h"
 
 #include <utility>
 
-typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
-typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
-
 namespace {
-
-constexpr float kLoInv = 1.f / 2048.f;
 
 struct SP {
   const float *x;
@@ -75,43 +71,12 @@ struct SP {
   int r2cs, r2co;
   int Wout;
   int vec, vec_out;
+  int direct;              // epilogue straight from the accumulators (no shuffle, 16-byte aligned pieces)
   int tiles_x, tiles_y, nblk, ntiles;
   int nchunks, tpk_last;   // taps per K step of the last chunk (1, 2 or 4)
   int64_t wchunk;          // halves of one full chunk's packed weights (hi + lo)
   int wbytes;              // bytes of the packed weights
 };
-
-// LDS images: a row is one pixel (or one (tap-row, n)) x 32 halves = 4 slots
-// of 16 bytes.  Weight rows: slot XOR {0, 2, 3, 1}[(row >> 2) & 3], read 16
-// consecutive rows from a multiple of 16: conflict-free ds_read_b128 lane
-// groups.  Input image: slot XOR 2 * ((x >> 2) & 1) of the pixel's column x
-// in its halo row (row pitch a multiple of 4 pixels): conflict-free for the
-// 16 consecutive pixels of a stride-1 tap at any column offset.
-__device__ __forceinline__ int swz(int row, int slot) {
-  const int x = (0x1320 >> (((row >> 2) & 3) << 2)) & 3;
-  return row * 32 + ((slot ^ x) << 3);
-}
-__device__ __forceinline__ int swzx(int row, int x, int slot) {
-  return row * 32 + ((slot ^ (((x >> 2) & 1) << 1)) << 3);
-}
-
-__device__ __forceinline__ uint32_t pk(float a, float b) {
-  return __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(a, b));
-}
-
-// 8 fp32 values -> (hi, lo) fp16 pieces; see the header for the split.  hi is
-// the fp16 value of v rounded toward zero (exact below fp16's normal range
-// too: the remainder is taken from hi's own fp32 value), lo = (v - hi) * 2^11
-// (v - hi is exact in fp32), rounded toward zero to fp16
-__device__ __forceinline__ void split8(const float v[8], u32x4_t &h, u32x4_t &l) {
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const auto hh = __builtin_amdgcn_cvt_pkrtz(v[2 * j], v[2 * j + 1]);
-    const float h0 = (float)hh[0], h1 = (float)hh[1];
-    h[j] = __builtin_bit_cast(uint32_t, hh);
-    l[j] = pk((v[2 * j] - h0) * 2048.f, (v[2 * j + 1] - h1) * 2048.f);
-  }
-}
 
 // RES = false: weights streamed one kernel row (KS taps) of one chunk per
 // stage by LDS-DMA into two buffers; RES = true: every weight row of the
@@ -149,22 +114,6 @@ struct SG {
 // rows of the packed weights of a chunk with tpk taps per K step
 __device__ __forceinline__ int chunk_rows(int kt, int tpk) { return (kt + tpk - 1) / tpk; }
 
-__device__ __forceinline__ void wait_vm_lgkm() { __builtin_amdgcn_s_waitcnt(0x0070); }   // vmcnt(0) lgkmcnt(0)
-// vmcnt(N) lgkmcnt(0): all but the N youngest vector-memory operations done
-template <int N>
-__device__ __forceinline__ void wait_vm_n_lgkm() {
-  static_assert(N >= 0 && N < 64, "vmcnt is 6 bits");
-  __builtin_amdgcn_s_waitcnt(0x0070 | (N & 15) | ((N >> 4) << 14));
-}
-// workgroup barrier without the vmcnt(0) __syncthreads() implies while an
-// LDS-DMA is in flight; LDS ordering is made explicit by the callers' waits
-__device__ __forceinline__ void raw_barrier() {
-  asm volatile("" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-}
-__device__ __forceinline__ void wait_lgkm() { __builtin_amdgcn_s_waitcnt(0xC07F); }      // lgkmcnt(0)
-
 template <int KS, int S, int BN, int RW, int NW, bool GATE, bool RES>
 __global__ void __launch_bounds__(NW * 64) sconv_kernel(SP p) {
   typedef SG<KS, S, BN, RW, NW, RES> G_;
@@ -193,18 +142,21 @@ __global__ void __launch_bounds__(NW * 64) sconv_kernel(SP p) {
   const int spc_last = (chunk_rows(KT, p.tpk_last) + RG - 1) / RG;
   const int nstages = (p.nchunks - 1) * spc_full + spc_last;
 
-  // image piece plan (constant): piece u = (halo pixel, 8-channel slot)
-  int ipix[PPI], iofs[PPI];
+  // image piece plan (constant): piece u = (halo pixel, 8-channel slot);
+  // prel = its element offset from the tile's first halo pixel
+  int ipix[PPI], iofs[PPI], prel[PPI];
 #pragma unroll
   for (int u = 0; u < PPI; ++u) {
     const int it = tid + u * kNT;
     ipix[u] = -1;
     iofs[u] = 0;
+    prel[u] = 0;
     if (it < IH * IW * 4) {
       const int slot = it & 3, pix = it >> 2;
       const int iy = pix / IW, ix = pix - iy * IW;
       ipix[u] = (iy << 16) | (ix << 2) | slot;
       iofs[u] = swzx(iy * IWP + ix, ix, slot);
+      prel[u] = (iy * p.W + ix) * p.xcs + slot * 8;
     }
   }
   float pfi[PPI][8];
@@ -218,9 +170,14 @@ __global__ void __launch_bounds__(NW * 64) sconv_kernel(SP p) {
     ox0 = (sp % p.tiles_x) * 16;
   };
   auto stage_of = [&](int s, int &c, int &r0, int &tpk) {
-    c = s / spc_full;
-    if (c > p.nchunks - 1) c = p.nchunks - 1;
-    r0 = (s - c * spc_full) * RG;
+    if constexpr (RES) {
+      c = s;
+      r0 = 0;
+    } else {
+      c = s / spc_full;
+      if (c > p.nchunks - 1) c = p.nchunks - 1;
+      r0 = (s - c * spc_full) * RG;
+    }
     tpk = c == p.nchunks - 1 ? p.tpk_last : 1;
   };
   // registers <- global: the input pieces of chunk c of tile t.  Buffer
@@ -239,13 +196,14 @@ __global__ void __launch_bounds__(NW * 64) sconv_kernel(SP p) {
     const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<float *>(p.x + eb), (short)0, (int)nrec, 0x00020000);
     const int cl = p.cin - c * 32;   // channels of this chunk left in the input
+    const int toff = ((iy0 - rb) * p.W + ix0) * p.xcs;   // the tile's first halo pixel, from the base
 #pragma unroll
     for (int u = 0; u < PPI; ++u) {
       const int q = ipix[u];
       const int gy = iy0 + (q >> 16), gx = ix0 + ((q >> 2) & 0x3fff);
       const int c0 = (q & 3) * 8;
-      const bool in = q >= 0 && gy >= 0 && gy < p.H && gx >= 0 && gx < p.W;
-      const int off = ((gy - rb) * p.W + gx) * p.xcs + c0;   // elements from the base
+      const bool in = q >= 0 && (unsigned)gy < (unsigned)p.H && (unsigned)gx < (unsigned)p.W;
+      const int off = toff + prel[u];   // elements from the base
       if (p.vec) {
         const int o = in && c0 < cl ? off * 4 : 0x7fffffe0;
         const f32x4 a = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, o, 0, 0));
@@ -413,7 +371,10 @@ __global__ void __launch_bounds__(NW * 64) sconv_kernel(SP p) {
       const int nr = rows - r0 < RG ? rows - r0 : RG;
       const int spt = 4 / tpk;
       const int sub = hi / spt, slot = hi - sub * spt;
-      for (int rr = 0; rr < nr; ++rr) {
+      constexpr int RMAX = RG < (KT + 1) / 2 ? RG : (KT + 1) / 2;   // rows of a stage with >= 2 taps per row
+#pragma unroll
+      for (int rr = 0; rr < RMAX; ++rr) {
+        if (rr >= nr) break;
         int tap = tpk * (r0 + rr) + sub;
         if (tap >= KT) tap = 0;  // zero weights, any finite data
         const int dy = tap / KS, dx = tap - dy * KS;
@@ -490,6 +451,60 @@ __global__ void __launch_bounds__(NW * 64) sconv_kernel(SP p) {
         else if (more) prefetch_img(t + G, 0), img_inflight = true;
       }
       compute(s, k & 1);
+    }
+    if (p.direct) {
+      // epilogue straight from the accumulators: lane (col, hi) of fragment
+      // (r, j) holds output channels n0 + 16 j + 4 hi .. + 3 of pixel (row
+      // wave * RW + r, column col); out = scale * (res2 + (res + act(acc +
+      // bias))) in the reference's order, 16-byte loads and stores
+#pragma unroll
+      for (int r = 0; r < RW; ++r) {
+        const int oy = oy0 + wave * RW + r, ox = ox0 + col;
+        const bool okp = oy < p.Ho && ox < p.Wo;
+        const int64_t pix = (int64_t)oy * p.Wout + ox;
+        f32x4 r1[NT], r2[NT];
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+          const int n = n0 + j * 16 + hi * 4;
+          const bool ok = okp && n < p.cout;
+          r1[j] = (p.res && ok) ? *reinterpret_cast<const f32x4 *>(reinterpret_cast<const float *>(p.res) +
+                                                                  pix * p.rcs + p.rco + n)
+                                : f32x4{0.f, 0.f, 0.f, 0.f};
+          r2[j] = (p.res2 && ok) ? *reinterpret_cast<const f32x4 *>(reinterpret_cast<const float *>(p.res2) +
+                                                                   pix * p.r2cs + p.r2co + n)
+                                 : f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+          const int nl = j * 16 + hi * 4, n = n0 + nl;
+          const float4 bb = *reinterpret_cast<const float4 *>(Lc + nl);
+          const float4 sc = *reinterpret_cast<const float4 *>(Lc + BN + nl);
+          f32x4 v;
+          v[0] = (am[r][j][0] + ac[r][j][0] * kLoInv) + bb.x;
+          v[1] = (am[r][j][1] + ac[r][j][1] * kLoInv) + bb.y;
+          v[2] = (am[r][j][2] + ac[r][j][2] * kLoInv) + bb.z;
+          v[3] = (am[r][j][3] + ac[r][j][3] * kLoInv) + bb.w;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = apply_act(p.act, v[e], p.slope);
+          if (p.res) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = r1[j][e] + v[e];
+          }
+          if (p.res2) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = r2[j][e] + v[e];
+          }
+          if (p.scale) {
+            v[0] *= sc.x;
+            v[1] *= sc.y;
+            v[2] *= sc.z;
+            v[3] *= sc.w;
+          }
+          if (okp && n < p.cout)
+            *reinterpret_cast<f32x4 *>(reinterpret_cast<float *>(p.y) + pix * p.ycs + p.yco + n) = v;
+        }
+      }
+      continue;
     }
     wait_lgkm();
     raw_barrier();     // every wave is done reading the image: T may overwrite it
@@ -607,23 +622,36 @@ int try_bn(SP p, int bn, hipStream_t st) {
   }
 }
 
+// dcvc_set_option("sconv_res_waves", 4 | 8 | 0 = auto): waves per workgroup of
+// the resident kernels; auto = 8 for 3x3 (two waves per SIMD hide each
+// other's LDS and VALU phases: 48->48 at 1080p 548 -> 465 us), 4 for 1x1
+// (a wave per SIMD with the whole register file: 48->192 at 1080p 2300 ->
+// 1056 us)
+int g_res_waves = 0;
+
 template <int KS, int S, bool GATE>
 int pick_bn(SP p, hipStream_t st) {
   int order[4];
   if constexpr (KS != 7) {
-    // resident weights (one wave per SIMD, AGPR accumulators) where they fit
+    // resident weights where they fit
     if (g_resident) {
       bn_order(p.cout, 64, order);
       for (int i = 0; i < 4 && order[i]; ++i) {
-        const int r = try_bn<KS, S, GATE, true, 4>(p, order[i], st);
+        const int nw = g_res_waves ? g_res_waves : (KS == 1 ? 4 : 8);
+        const int r = nw == 4 ? try_bn<KS, S, GATE, true, 4>(p, order[i], st)
+                              : try_bn<KS, S, GATE, true, 8>(p, order[i], st);
         if (r != DCVC_HIP_EUNSUPPORTED) return r;
       }
     }
   }
-  // streamed weights; 7x7 layers stay <= 32 channels per n-block
-  bn_order(p.cout, KS == 7 ? 32 : 64, order);
-  if (g_waves == 4) return try_bn<KS, S, GATE, false, 4>(p, order[0], st);
-  return try_bn<KS, S, GATE, false, 8>(p, order[0], st);
+  if constexpr (KS == 1) {
+    return DCVC_HIP_EUNSUPPORTED;   // (a 1x1 n-block of 16 channels always fits resident)
+  } else {
+    // streamed weights; 7x7 layers stay <= 32 channels per n-block
+    bn_order(p.cout, KS == 7 ? 32 : 64, order);
+    if (g_waves == 4) return try_bn<KS, S, GATE, false, 4>(p, order[0], st);
+    return try_bn<KS, S, GATE, false, 8>(p, order[0], st);
+  }
 }
 
 }  // namespace
@@ -631,6 +659,7 @@ int pick_bn(SP p, hipStream_t st) {
 extern "C" void dcvc_internal_sconv_occupancy(int v) { g_occ = v; }
 extern "C" void dcvc_internal_sconv_waves(int v) { g_waves = v; }
 extern "C" void dcvc_internal_sconv_resident(int v) { g_resident = v; }
+extern "C" void dcvc_internal_sconv_res_waves(int v) { g_res_waves = v; }
 
 // f16x3 convolutions (a->compute == DCVC_F16X3): fp32 input and output views.
 // Kernel sizes 1, 3 (stride 1 or 2) and 7 (stride 1); the ConvFFN2 gate input
@@ -679,6 +708,11 @@ extern "C" int dcvc_internal_sconv(const dcvc_conv_args *a, void *stream) {
     if (a->res.ptr) vo = vo && (p.rcs % 8 == 0) && (p.rco % 8 == 0) && ((uintptr_t)p.res % 16 == 0);
     if (a->res2.ptr) vo = vo && (p.r2cs % 8 == 0) && (p.r2co % 8 == 0) && ((uintptr_t)p.res2 % 16 == 0);
     p.vec_out = vo ? 1 : 0;
+    // the direct epilogue stores 4 channels per lane: needs cout % 4 == 0 and
+    // 16-byte aligned output / residual pieces
+    p.direct = !a->shuffle && a->cout % 4 == 0 && (p.ycs % 4 == 0) && (p.yco % 4 == 0) && ((uintptr_t)p.y % 16 == 0);
+    if (a->res.ptr) p.direct = p.direct && (p.rcs % 4 == 0) && (p.rco % 4 == 0) && ((uintptr_t)p.res % 16 == 0);
+    if (a->res2.ptr) p.direct = p.direct && (p.r2cs % 4 == 0) && (p.r2co % 4 == 0) && ((uintptr_t)p.res2 % 16 == 0);
   }
   p.nchunks = (a->cin + 31) / 32;
   const int vc = a->cin - 32 * (p.nchunks - 1);

@@ -1,0 +1,102 @@
+// Split-fp16 ("f16x3") helpers shared by the kernels of Precision.split()
+// (sconv.hip, sffn.hip) and the host packers (conv.hip, sffn.hip): an fp32
+// value a is carried as two fp16 values, a = hi + 2^-11 lo, and a product as
+// three f16 MFMAs, xh * wh + 2^-11 (xh * wl + xl * wh) (sconv.hip's header).
+#pragma once
+#include "common.h"
+
+#include <cmath>
+#include <cstring>
+
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+
+// LDS images: a row is one pixel (or one (tap-row, n)) x 32 halves = 4 slots
+// of 16 bytes.  Weight rows: slot XOR {0, 2, 3, 1}[(row >> 2) & 3], read 16
+// consecutive rows from a multiple of 16: conflict-free ds_read_b128 lane
+// groups.  Input image: slot XOR 2 * ((x >> 2) & 1) of the pixel's column x
+// in its halo row (row pitch a multiple of 4 pixels): conflict-free for the
+// 16 consecutive pixels of a stride-1 tap at any column offset.
+__device__ __forceinline__ int swz(int row, int slot) {
+  const int x = (0x1320 >> (((row >> 2) & 3) << 2)) & 3;
+  return row * 32 + ((slot ^ x) << 3);
+}
+__device__ __forceinline__ int swzx(int row, int x, int slot) {
+  return row * 32 + ((slot ^ (((x >> 2) & 1) << 1)) << 3);
+}
+
+__device__ __forceinline__ uint32_t pk(float a, float b) {
+  return __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(a, b));
+}
+
+// 8 fp32 values -> (hi, lo) fp16 pieces; see the header for the split.  hi is
+// the fp16 value of v rounded toward zero (exact below fp16's normal range
+// too: the remainder is taken from hi's own fp32 value), lo = (v - hi) * 2^11
+// (v - hi is exact in fp32), rounded toward zero to fp16
+__device__ __forceinline__ void split8(const float v[8], u32x4_t &h, u32x4_t &l) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const auto hh = __builtin_amdgcn_cvt_pkrtz(v[2 * j], v[2 * j + 1]);
+    const float h0 = (float)hh[0], h1 = (float)hh[1];
+    h[j] = __builtin_bit_cast(uint32_t, hh);
+    l[j] = pk((v[2 * j] - h0) * 2048.f, (v[2 * j + 1] - h1) * 2048.f);
+  }
+}
+
+constexpr float kLoInv = 1.f / 2048.f;
+
+__device__ __forceinline__ void wait_vm_lgkm() { __builtin_amdgcn_s_waitcnt(0x0070); }   // vmcnt(0) lgkmcnt(0)
+// vmcnt(N) lgkmcnt(0): all but the N youngest vector-memory operations done
+template <int N>
+__device__ __forceinline__ void wait_vm_n_lgkm() {
+  static_assert(N >= 0 && N < 64, "vmcnt is 6 bits");
+  __builtin_amdgcn_s_waitcnt(0x0070 | (N & 15) | ((N >> 4) << 14));
+}
+// workgroup barrier without the vmcnt(0) __syncthreads() implies while an
+// LDS-DMA is in flight; LDS ordering is made explicit by the callers' waits
+__device__ __forceinline__ void raw_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+__device__ __forceinline__ void wait_lgkm() { __builtin_amdgcn_s_waitcnt(0xC07F); }      // lgkmcnt(0)
+
+// host f32 -> f16, round to nearest even (subnormals kept; |v| < 65520 assumed)
+static inline uint16_t host_f2h(float v) {
+  uint32_t u;
+  std::memcpy(&u, &v, 4);
+  const uint32_t sign = (u >> 16) & 0x8000u;
+  const int e = (int)((u >> 23) & 0xff) - 127;
+  uint32_t m = u & 0x7fffffu;
+  if (e > 15) return (uint16_t)(sign | 0x7c00u);          // overflow: infinity
+  if (e >= -14) {                                         // normal f16
+    uint32_t h = ((uint32_t)(e + 15) << 10) | (m >> 13);
+    const uint32_t rest = m & 0x1fffu;
+    if (rest > 0x1000u || (rest == 0x1000u && (h & 1u))) ++h;  // may carry into the exponent: still correct
+    return (uint16_t)(sign | h);
+  }
+  if (e < -25) return (uint16_t)sign;                     // below half the smallest subnormal
+  m |= 0x800000u;                                         // subnormal f16: value = m * 2^(e - 23)
+  const int shift = -e - 1;                               // 14..24: keep m >> shift as units of 2^-24
+  uint32_t h = m >> shift;
+  const uint32_t rest = m & ((1u << shift) - 1u), half = 1u << (shift - 1);
+  if (rest > half || (rest == half && (h & 1u))) ++h;
+  return (uint16_t)(sign | h);
+}
+static inline float host_h2f(uint16_t h) {
+  const int e = (h >> 10) & 0x1f;
+  const uint32_t m = h & 0x3ffu;
+  float f;
+  if (e == 0) {
+    f = std::ldexp((float)m, -24);
+  } else {
+    uint32_t u = ((uint32_t)(e - 15 + 127) << 23) | (m << 13);
+    std::memcpy(&f, &u, 4);
+  }
+  return (h & 0x8000u) ? -f : f;
+}
+// w = hi + 2^-11 lo: hi = f16(w), lo = f16((w - hi) * 2^11)
+static inline void host_split(float w, uint16_t &hi, uint16_t &lo) {
+  hi = host_f2h(w);
+  lo = host_f2h((w - host_h2f(hi)) * 2048.f);
+}

@@ -18,6 +18,7 @@ msssim.hip), pinned to the reference's outputs.  RGB MS-SSIM is
 from this image: ``MsSsimRGB`` follows its published algorithm on the GPU and
 the log carries ``msssim_unpinned``.
 """
+import contextlib
 import os
 import time
 
@@ -377,12 +378,25 @@ class ReconWriter:
         self.file.write(np.clip(np.rint(uv * 255), 0, 255).astype(np.uint8).tobytes())
 
     def close(self):
-        for j in self.jobs:
-            j.result()
-        self.jobs = []
-        self.pool.shutdown()
-        if self.file is not None:
-            self.file.close()
+        """Drain the writer thread and close out.yuv (idempotent)."""
+        try:
+            for j in self.jobs:
+                j.result()
+        finally:
+            self.jobs = []
+            self.pool.shutdown()
+            if self.file is not None:
+                self.file.close()
+                self.file = None
+
+    # run_test holds the writer in a `with`: on an exception mid-sequence the
+    # queued frames are still written and the file closed
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+        return False
 
 
 def psnr_rgb(sse3, h, w):
@@ -513,7 +527,7 @@ def run_test(p_frame_net, i_frame_net, args):
     p_frame_number = 0
     enc_t = dec_t = 0.0
     dpb = None
-    with torch.no_grad():
+    with torch.no_grad(), (writer if writer is not None else contextlib.nullcontext()):
         for frame_idx in range(frame_num):
             frame = reader.read_one_frame(dst_format="420" if yuv else "rgb")
             if frame is None or (yuv and frame[0] is None):
@@ -550,8 +564,6 @@ def run_test(p_frame_net, i_frame_net, args):
                 writer.write(recon, frame_idx)
             if verbose >= 2:
                 print(f"frame {frame_idx}, bits: {bits[-1]:.3f}", flush=True)
-    if writer is not None:
-        writer.close()
     sse = stage.sums()
     test_time = time.time() - start_time
     if verbose >= 1 and p_frame_number > 0:
@@ -608,7 +620,7 @@ def run_test_hem(video_net, i_frame_net, args, device=None):
     frame_types, bits = [], []
     start_time = time.time()
     dpb = None
-    with torch.no_grad():
+    with torch.no_grad(), (writer if writer is not None else contextlib.nullcontext()):
         for frame_idx in range(frame_num):
             frame = reader.read_one_frame(dst_format="rgb")
             if frame is None:
@@ -635,8 +647,6 @@ def run_test_hem(video_net, i_frame_net, args, device=None):
                 ms.run(as_act(recon), dframe, frame_idx)
             if writer is not None:
                 writer.write(recon, frame_idx)
-    if writer is not None:
-        writer.close()
     sse = stage.sums()
     psnrs = [psnr_rgb(sse[i], h, w) for i in range(frame_num)]
     mv = ms.values(frame_num) if ms is not None else [0.0] * frame_num

@@ -51,6 +51,12 @@ class CConvArgs(ctypes.Structure):
                 ("res", CTensor), ("res2", CTensor)]
 
 
+class CFfnArgs(ctypes.Structure):
+    _fields_ = [("x", CTensor), ("y", CTensor), ("c", ctypes.c_int), ("hidden", ctypes.c_int),
+                ("w", ctypes.c_void_p), ("b1", ctypes.c_void_p), ("b2", ctypes.c_void_p),
+                ("scale", ctypes.c_void_p), ("slope", ctypes.c_float)]
+
+
 _T = CTensor
 _vp, _i, _f = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
 HIP_SYMBOLS = [
@@ -59,6 +65,8 @@ HIP_SYMBOLS = [
     ("dcvc_set_option", _i, [ctypes.c_char_p, _i]),
     ("dcvc_last_kernel", ctypes.c_char_p, []),
     ("dcvc_depthconv_block", _i, [ctypes.POINTER(CDcbArgs), _vp]),
+    ("dcvc_ffn_pack_weights", ctypes.c_int64, [_vp, _vp, _i, _i, _vp]),
+    ("dcvc_conv_ffn", _i, [ctypes.POINTER(CFfnArgs), _vp]),
     ("dcvc_dwconv3x3", _i, [_T, _T, _vp, _vp, _vp]),
     ("dcvc_flow_warp", _i, [_T, _T, _T, _vp, _vp, _vp]),
     ("dcvc_offset_diversity", _i, [_T, _T, _T, _T, _vp, _vp, _vp, _vp, _f, _vp]),
@@ -381,6 +389,50 @@ def conv(cw, x, y=None, *, out_dtype=None, in_op=IN_NONE, in_slope=0.0, act=ACT_
 
 
 UNSUPPORTED = -3
+
+
+class FfnW:
+    """A ConvFFN's weights packed for the fused split-fp16 kernel (sffn.hip):
+    w1 = conv.0 [hidden][c][1][1], w2 = conv.2 [c][hidden][1][1]."""
+
+    def __init__(self, w1, b1, w2, b2, device=None):
+        w1 = w1.detach().float().cpu().reshape(w1.shape[0], -1).contiguous().numpy()
+        w2 = w2.detach().float().cpu().reshape(w2.shape[0], -1).contiguous().numpy()
+        self.hidden, self.c = w1.shape
+        vp = ctypes.c_void_p
+        n = int(lib().dcvc_ffn_pack_weights(w1.ctypes.data_as(vp), w2.ctypes.data_as(vp), self.c, self.hidden, None))
+        check(n, "ffn_pack_weights")
+        host = np.zeros(n, dtype=np.uint16)
+        check(int(lib().dcvc_ffn_pack_weights(w1.ctypes.data_as(vp), w2.ctypes.data_as(vp), self.c, self.hidden,
+                                               host.ctypes.data_as(vp))), "ffn_pack_weights")
+        dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
+        self.w = torch.from_numpy(host.view(np.int16)).to(dev)
+        self.b1 = b1.detach().float().contiguous().to(dev)
+        self.b2 = b2.detach().float().contiguous().to(dev)
+
+
+def conv_ffn(fw, x, y=None, scale=None, slope=0.1):
+    """y = scale * (x + lrelu(ffn2(lrelu(ffn1(x) + b1)) + b2)) in one kernel
+    (dcvc_conv_ffn); None when no kernel is instantiated for the shape."""
+    if y is None:
+        y = empty(x.H, x.W, x.C, F32, x.buf.device)
+    a = CFfnArgs()
+    a.x, a.y = x.c(), y.c()
+    a.c, a.hidden = fw.c, fw.hidden
+    a.w, a.b1, a.b2 = fw.w.data_ptr(), fw.b1.data_ptr(), fw.b2.data_ptr()
+    a.scale = scale.data_ptr() if scale is not None else None
+    a.slope = slope
+    e0 = _t0()
+    r = lib().dcvc_conv_ffn(ctypes.byref(a), stream())
+    if r == UNSUPPORTED:
+        return None
+    check(r, "conv_ffn")
+    if e0 is not None:
+        n = x.H * x.W
+        kname = lib().dcvc_last_kernel().decode()
+        _t1(e0, kname.split("<")[0], 4 * n * fw.c * fw.hidden, n * fw.c * 4 * 3 + fw.w.numel() * 2,
+            f"{kname} | ffn {fw.c}->{fw.hidden}->{fw.c} {x.H}x{x.W} f16x3")
+    return y
 
 
 def depthconv_block(blk, x, y, scale=None):

@@ -24,6 +24,7 @@ from .hip import Act, F32, BF16, F16X3, ACT_LRELU, ACT_NONE, IN_LRELU, IN_GATE
 
 
 FUSE_DCB = True   # fused DepthConvBlock kernel where instantiated (A/B switch)
+FUSE_FFN = True   # split precision: fused ConvFFN kernel (sffn.hip) where instantiated (A/B switch)
 
 
 class Precision:
@@ -148,6 +149,14 @@ class DepthConvBlock:
             self.ffn1 = ctx.conv(f + ".conv.0", latent=latent)
             self.ffn2 = ctx.conv(f + ".conv.2", latent=latent)
         self.cout = self.ffn2.cout
+        # split precision: the ConvFFN as one fused kernel (sffn.hip) where one
+        # is instantiated for its width; the hidden layer stays in LDS
+        self.ffn = None
+        if (FUSE_FFN and not gated and self.ffn2.compute == F16X3 and self.cout in (32, 48, 64, 128)
+                and self.ffn1.cout % (32 if self.cout >= 128 else 64) == 0):
+            sd = ctx.sd
+            self.ffn = K.FfnW(sd[f + ".conv.0.weight"], sd[f + ".conv.0.bias"], sd[f + ".conv.2.weight"],
+                              sd[f + ".conv.2.bias"], ctx.dev)
 
     def __call__(self, x, y=None, scale=None):
         ctx = self.ctx
@@ -168,6 +177,10 @@ class DepthConvBlock:
         if self.gated:
             h = K.conv(self.ffn1, dc)
             return K.conv(self.ffn2, h, y, in_op=IN_GATE, in_slope=self.slope_ffn, res=dc, scale=scale)
+        if self.ffn is not None:
+            out = K.conv_ffn(self.ffn, dc, y, scale=scale, slope=self.slope_ffn)
+            if out is not None:
+                return out
         # the hidden layer feeds only ffn2: with bf16 compute ffn2 rounds it
         # to bf16 on staging anyway, so it is stored as bf16 (same values,
         # half the traffic of the 4x-wide map)

@@ -135,6 +135,28 @@ typedef struct dcvc_dcb_args {
 } dcvc_dcb_args;
 int dcvc_depthconv_block(const dcvc_dcb_args *a, void *stream);
 
+/*
+ * Fused ConvFFN in split-fp16 arithmetic (Precision.split()),
+ * DCVC-DC/src/models/layers.py:166-179 with the DepthConvBlock's optional
+ * output scale:  y = scale * (x + lrelu(ffn2(lrelu(ffn1(x) + b1)) + b2)),
+ * lrelu slope `slope` (0.1), fp32 views of c channels (c in {32, 48, 64, 128},
+ * hidden a multiple of 64, or of 32 for c = 128); the hidden layer never
+ * leaves LDS.  Weights packed by dcvc_ffn_pack_weights from w1 = conv.0
+ * [hidden][c] and w2 = conv.2 [c][hidden] (fp32, host); out NULL returns the
+ * element count.  DCVC_HIP_EUNSUPPORTED for other shapes (the caller runs
+ * the two convs).
+ */
+typedef struct dcvc_ffn_args {
+  dcvc_tensor x, y;
+  int c, hidden;
+  const void *w;
+  const float *b1, *b2;
+  const float *scale;     /* [c] or NULL */
+  float slope;
+} dcvc_ffn_args;
+int64_t dcvc_ffn_pack_weights(const float *w1, const float *w2, int c, int hidden, void *out);
+int dcvc_conv_ffn(const dcvc_ffn_args *a, void *stream);
+
 /* Depthwise 3x3 conv, stride 1, padding 1, + bias (DepthConv.depth_conv,
  * DCVC-DC/src/models/layers.py:143-144).  w: [9][C] fp32 (tap-major). */
 int dcvc_dwconv3x3(dcvc_tensor x, dcvc_tensor y, const float *w,

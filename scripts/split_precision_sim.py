@@ -58,7 +58,7 @@ def make_conv(mode, feat_min_hw):
         c = lambda a, ww: Fn.conv2d(a, ww, None, stride=stride, padding=pad)  # noqa: E731
         if mode == "bf16":
             out = c(x.bfloat16().float(), w.bfloat16().float())
-        elif mode in ("bf16x3", "fp16x3", "fp16x3s", "fp16x3w", "bf16x2w"):
+        elif mode in ("bf16x3", "fp16x3", "fp16x3s", "fp16x3w", "bf16x2w", "fp16x2w", "fp16x2x"):
             dt = torch.bfloat16 if mode.startswith("bf16") else torch.float16
             sx = sw = 1.0
             if mode == "fp16x3s":
@@ -67,8 +67,10 @@ def make_conv(mode, feat_min_hw):
                 sw = pow2_scale(w)
             xh, xl = split(x * sx, dt)
             wh, wl = split(w * sw, dt)
-            if mode == "bf16x2w":     # activations hi only, weights split
+            if mode in ("bf16x2w", "fp16x2w"):     # activations hi only, weights split
                 out = c(xh, wh) + c(xh, wl)
+            elif mode == "fp16x2x":               # weights hi only, activations split
+                out = c(xh, wh) + c(xl, wh)
             else:
                 out = c(xh, wh) + (c(xh, wl) + c(xl, wh))
             out = out * (1.0 / (sx * sw))

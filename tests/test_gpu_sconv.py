@@ -142,3 +142,30 @@ def test_sconv_fp16_subnormal_operands():
     y = h.conv(h.ConvW(w, torch.zeros(32), 1, h.F16X3), h.from_nchw(x, h.F32), out_dtype=h.F32)
     torch.cuda.synchronize()
     assert rel_err(y.nchw().cpu(), ref) < 1e-4
+
+
+@pytest.mark.parametrize("c,H,W", [(48, 37, 53), (32, 20, 70), (64, 33, 31), (128, 17, 30)])
+def test_fused_ffn_matches_fp64(c, H, W):
+    """sffn.hip: out = scale * (x + lrelu(ffn2(lrelu(ffn1(x) + b1)) + b2))
+    (ConvFFN, DCVC-DC/src/models/layers.py:166-179) in one kernel, on channel
+    views, against fp64."""
+    h = K()
+    g = torch.Generator().manual_seed(c + H)
+    hid = 4 * c
+    big = torch.randn(1, c + 8, H, W, generator=g)
+    x = big[:, 4:4 + c]
+    w1 = torch.randn(hid, c, 1, 1, generator=g) / c ** 0.5
+    b1 = torch.randn(hid, generator=g) * 0.1
+    w2 = torch.randn(c, hid, 1, 1, generator=g) / hid ** 0.5
+    b2 = torch.randn(c, generator=g) * 0.1
+    sc = torch.rand(c, generator=g) + 0.5
+    xd = x.double()
+    hh = F.leaky_relu(F.conv2d(xd, w1.double(), b1.double()), 0.1)
+    ref = (xd + F.leaky_relu(F.conv2d(hh, w2.double(), b2.double()), 0.1)) * sc.double().view(1, -1, 1, 1)
+    fw = h.FfnW(w1, b1, w2, b2)
+    xa = h.from_nchw(big, h.F32).ch(4, c)
+    out = h.empty(H, W, c + 8, h.F32)
+    y = h.conv_ffn(fw, xa, out.ch(4, c), scale=sc.cuda(), slope=0.1)
+    torch.cuda.synchronize()
+    assert y is not None and h.lib().dcvc_last_kernel().decode().startswith("sffn_kernel")
+    assert rel_err(out.ch(4, c).nchw().cpu(), ref) < TOL

@@ -67,3 +67,50 @@ def test_pack_f16x3_hi_is_round_to_nearest():
     buf = pack(w)
     hi = buf[:4 * 32].view(np.float16).reshape(4, 32)[:, 0].astype(np.float64)
     assert hi.tolist() == [1.0, 1.0 + 4 * 2 ** -11, float(np.float16(-0.1)), 64992.0]
+
+
+@pytest.mark.parametrize("c,hid", [(48, 192), (128, 512), (32, 128)])
+def test_ffn_pack_roundtrip(c, hid):
+    """dcvc_ffn_pack_weights: per hidden slice the swizzled LDS images of
+    ffn1 ([kc][h][32]) and ffn2 ([kc2][n][32]), hi then lo; decoded back they
+    give the weights to ~2^-22."""
+    from dcvc_amd import hip as h
+    g = torch.Generator().manual_seed(c)
+    w1 = (torch.randn(hid, c, generator=g) / c ** 0.5).numpy().astype(np.float32)
+    w2 = (torch.randn(c, hid, generator=g) / hid ** 0.5).numpy().astype(np.float32)
+    vp = ctypes.c_void_p
+    n = h.lib().dcvc_ffn_pack_weights(w1.ctypes.data_as(vp), w2.ctypes.data_as(vp), c, hid, None)
+    buf = np.zeros(n, dtype=np.uint16)
+    assert h.lib().dcvc_ffn_pack_weights(w1.ctypes.data_as(vp), w2.ctypes.data_as(vp), c, hid,
+                                         buf.ctypes.data_as(vp)) == n
+    HS = 32 if c >= 128 else 64
+    kc1, c16, kc2 = (c + 31) // 32, (c + 15) // 16 * 16, HS // 32
+    w1n, w2n = kc1 * HS * 32, kc2 * c16 * 32
+    sl = 2 * w1n + 2 * w2n
+    assert n == sl * (hid // HS)
+
+    def at(row, k):
+        x = (0x1320 >> (((row >> 2) & 3) << 2)) & 3
+        return row * 32 + ((((k >> 3) ^ x) & 3) << 3) + (k & 7)
+    f = buf.view(np.float16).astype(np.float64)
+    g1 = np.zeros((hid, c))
+    g2 = np.zeros((c, hid))
+    for s in range(hid // HS):
+        b = s * sl
+        for kc in range(kc1):
+            for hh in range(HS):
+                for k in range(32):
+                    ch = kc * 32 + k
+                    q = at(kc * HS + hh, k)
+                    v = f[b + q] + f[b + w1n + q] / 2048
+                    if ch < c:
+                        g1[s * HS + hh, ch] = v
+                    else:
+                        assert v == 0
+        for kc in range(kc2):
+            for nn in range(c):
+                for k in range(32):
+                    q = at(kc * c16 + nn, k)
+                    g2[nn, s * HS + kc * 32 + k] = f[b + 2 * w1n + q] + f[b + 2 * w1n + w2n + q] / 2048
+    for got, ref in ((g1, w1), (g2, w2)):
+        assert np.all(np.abs(got - ref) <= np.abs(ref) * 2.0 ** -21 + 2.0 ** -35)
