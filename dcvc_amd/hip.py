@@ -57,6 +57,12 @@ class CFfnArgs(ctypes.Structure):
                 ("scale", ctypes.c_void_p), ("slope", ctypes.c_float)]
 
 
+class CDcArgs(ctypes.Structure):
+    _fields_ = [("x", CTensor), ("y", CTensor), ("cin", ctypes.c_int), ("cout", ctypes.c_int),
+                ("adaptor", ctypes.c_int), ("w", ctypes.c_void_p), ("b1", ctypes.c_void_p), ("wdw", ctypes.c_void_p),
+                ("bdw", ctypes.c_void_p), ("b2", ctypes.c_void_p), ("ba", ctypes.c_void_p), ("slope", ctypes.c_float)]
+
+
 _T = CTensor
 _vp, _i, _f = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
 HIP_SYMBOLS = [
@@ -67,6 +73,8 @@ HIP_SYMBOLS = [
     ("dcvc_depthconv_block", _i, [ctypes.POINTER(CDcbArgs), _vp]),
     ("dcvc_ffn_pack_weights", ctypes.c_int64, [_vp, _vp, _i, _i, _vp]),
     ("dcvc_conv_ffn", _i, [ctypes.POINTER(CFfnArgs), _vp]),
+    ("dcvc_dc_pack_weights", ctypes.c_int64, [_vp, _vp, _vp, _i, _i, _vp]),
+    ("dcvc_depth_conv_split", _i, [ctypes.POINTER(CDcArgs), _vp]),
     ("dcvc_dwconv3x3", _i, [_T, _T, _vp, _vp, _vp]),
     ("dcvc_flow_warp", _i, [_T, _T, _T, _vp, _vp, _vp]),
     ("dcvc_offset_diversity", _i, [_T, _T, _T, _T, _vp, _vp, _vp, _vp, _f, _vp]),
@@ -409,6 +417,57 @@ class FfnW:
         self.w = torch.from_numpy(host.view(np.int16)).to(dev)
         self.b1 = b1.detach().float().contiguous().to(dev)
         self.b2 = b2.detach().float().contiguous().to(dev)
+
+
+class DcW:
+    """A DepthConv's weights packed for the fused split-fp16 kernel (sdc.hip):
+    conv1 [cin][cin], conv2 [cout][cin], adaptor [cout][cin] or None, the
+    depthwise taps w9c [9][cin] (device) and the biases."""
+
+    def __init__(self, w1, b1, w9c, bdw, w2, b2, wa=None, ba=None, device=None):
+        f = lambda w: w.detach().float().cpu().reshape(w.shape[0], -1).contiguous().numpy()  # noqa: E731
+        w1n, w2n = f(w1), f(w2)
+        wan = f(wa) if wa is not None else None
+        self.cin, self.cout = w1n.shape[0], w2n.shape[0]
+        vp = ctypes.c_void_p
+        pa = wan.ctypes.data_as(vp) if wan is not None else None
+        n = int(lib().dcvc_dc_pack_weights(w1n.ctypes.data_as(vp), w2n.ctypes.data_as(vp), pa, self.cin, self.cout,
+                                           None))
+        check(n, "dc_pack_weights")
+        host = np.zeros(n, dtype=np.uint16)
+        check(int(lib().dcvc_dc_pack_weights(w1n.ctypes.data_as(vp), w2n.ctypes.data_as(vp), pa, self.cin,
+                                             self.cout, host.ctypes.data_as(vp))), "dc_pack_weights")
+        dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
+        self.w = torch.from_numpy(host.view(np.int16)).to(dev)
+        g = lambda t: t.detach().float().contiguous().to(dev)  # noqa: E731
+        self.b1, self.w9c, self.bdw, self.b2 = g(b1), g(w9c), g(bdw), g(b2)
+        self.ba = g(ba) if wa is not None else None
+
+
+def depth_conv_split(dw, x, y=None, slope=0.01):
+    """DepthConv (conv1, LeakyReLU, depthwise 3x3, conv2, + identity) in one
+    kernel (dcvc_depth_conv_split); None when not instantiated for the shape."""
+    if y is None:
+        y = empty(x.H, x.W, dw.cout, F32, x.buf.device)
+    a = CDcArgs()
+    a.x, a.y = x.c(), y.c()
+    a.cin, a.cout, a.adaptor = dw.cin, dw.cout, 1 if dw.ba is not None else 0
+    a.w, a.b1, a.wdw, a.bdw, a.b2 = dw.w.data_ptr(), dw.b1.data_ptr(), dw.w9c.data_ptr(), dw.bdw.data_ptr(), \
+        dw.b2.data_ptr()
+    a.ba = dw.ba.data_ptr() if dw.ba is not None else None
+    a.slope = slope
+    e0 = _t0()
+    r = lib().dcvc_depth_conv_split(ctypes.byref(a), stream())
+    if r == UNSUPPORTED:
+        return None
+    check(r, "depth_conv_split")
+    if e0 is not None:
+        n = x.H * x.W
+        kname = lib().dcvc_last_kernel().decode()
+        fl = 2 * n * (dw.cin * dw.cin + 9 * dw.cin + dw.cin * dw.cout * (2 if dw.ba is not None else 1))
+        _t1(e0, kname.split("<")[0], fl, n * (dw.cin + dw.cout) * 4 + dw.w.numel() * 2,
+            f"{kname} | depthconv {dw.cin}->{dw.cout} {x.H}x{x.W} f16x3")
+    return y
 
 
 def conv_ffn(fw, x, y=None, scale=None, slope=0.1):

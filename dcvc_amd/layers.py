@@ -25,6 +25,9 @@ from .hip import Act, F32, BF16, F16X3, ACT_LRELU, ACT_NONE, IN_LRELU, IN_GATE
 
 FUSE_DCB = True   # fused DepthConvBlock kernel where instantiated (A/B switch)
 FUSE_FFN = True   # split precision: fused ConvFFN kernel (sffn.hip) where instantiated (A/B switch)
+FUSE_DC = True    # split precision: fused DepthConv kernel (sdc.hip) where instantiated (A/B switch)
+# (cin, cout, adaptor) of the fused DepthConv instantiations (sdc.hip supported())
+SDC_SHAPES = {(64, 48, True), (48, 32, True), (32, 64, True), (64, 64, False), (48, 48, False), (32, 32, False)}
 
 
 class Precision:
@@ -149,8 +152,17 @@ class DepthConvBlock:
             self.ffn1 = ctx.conv(f + ".conv.0", latent=latent)
             self.ffn2 = ctx.conv(f + ".conv.2", latent=latent)
         self.cout = self.ffn2.cout
-        # split precision: the ConvFFN as one fused kernel (sffn.hip) where one
-        # is instantiated for its width; the hidden layer stays in LDS
+        # split precision: DepthConv and ConvFFN as fused kernels (sdc.hip,
+        # sffn.hip) where one is instantiated for the block's widths; t1, the
+        # depthwise output and the 4x-wide hidden layer stay in LDS
+        self.dcw = None
+        sd = ctx.sd
+        if (FUSE_DC and self.conv1.compute == F16X3 and not latent and
+                (self.conv1.cin, self.conv2.cout, self.adaptor is not None) in SDC_SHAPES):
+            self.dcw = K.DcW(sd[d + ".conv1.0.weight"], sd[d + ".conv1.0.bias"], self.dw[0], self.dw[1],
+                             sd[d + ".conv2.weight"], sd[d + ".conv2.bias"],
+                             sd[d + ".adaptor.weight"] if self.adaptor is not None else None,
+                             sd[d + ".adaptor.bias"] if self.adaptor is not None else None, ctx.dev)
         self.ffn = None
         if (FUSE_FFN and not gated and self.ffn2.compute == F16X3 and self.cout in (32, 48, 64, 128)
                 and self.ffn1.cout % (32 if self.cout >= 128 else 64) == 0):
@@ -167,13 +179,19 @@ class DepthConvBlock:
             if K.depthconv_block(self, x, out, scale) is not None:
                 return out
         x = ctx.fit(x, self.conv1.compute)
-        if self.adaptor is not None:
+        dc = None
+        if self.dcw is not None:
+            dc = K.depth_conv_split(self.dcw, x, slope=self.slope_dc)
+        if dc is not None:
+            pass
+        elif self.adaptor is not None:
             idn = K.conv(self.adaptor, x, out_dtype=dt)
         else:
             idn = cast(x, dt)
-        t = K.conv(self.conv1, x, out_dtype=dt, act=ACT_LRELU, slope=self.slope_dc)
-        t = K.dwconv3x3(t, *self.dw)
-        dc = K.conv(self.conv2, t, res=idn)
+        if dc is None:
+            t = K.conv(self.conv1, x, out_dtype=dt, act=ACT_LRELU, slope=self.slope_dc)
+            t = K.dwconv3x3(t, *self.dw)
+            dc = K.conv(self.conv2, t, res=idn)
         if self.gated:
             h = K.conv(self.ffn1, dc)
             return K.conv(self.ffn2, h, y, in_op=IN_GATE, in_slope=self.slope_ffn, res=dc, scale=scale)

@@ -157,6 +157,26 @@ typedef struct dcvc_ffn_args {
 int64_t dcvc_ffn_pack_weights(const float *w1, const float *w2, int c, int hidden, void *out);
 int dcvc_conv_ffn(const dcvc_ffn_args *a, void *stream);
 
+/*
+ * Fused DepthConv in split-fp16 arithmetic (Precision.split()),
+ * DCVC-DC/src/models/layers.py:135-163:
+ *   y = conv2(dw3x3(lrelu(conv1(x) + b1, slope) + ...) + bdw) + b2 + identity,
+ * identity = adaptor(x) + ba (adaptor != 0) or x; the depthwise conv zero-pads
+ * t1 = lrelu(conv1(x) + b1).  fp32 views; (cin, cout) in {(64, 48), (48, 32),
+ * (32, 64) with adaptor; (64, 64), (48, 48), (32, 32) without}.  Weights
+ * packed by dcvc_dc_pack_weights from conv1 [cin][cin], conv2 [cout][cin] and
+ * the adaptor [cout][cin] (NULL without); wdw [9][cin] (tap-major) fp32.
+ */
+typedef struct dcvc_dc_args {
+  dcvc_tensor x, y;
+  int cin, cout, adaptor;
+  const void *w;
+  const float *b1, *wdw, *bdw, *b2, *ba;
+  float slope;
+} dcvc_dc_args;
+int64_t dcvc_dc_pack_weights(const float *w1, const float *w2, const float *wa, int cin, int cout, void *out);
+int dcvc_depth_conv_split(const dcvc_dc_args *a, void *stream);
+
 /* Depthwise 3x3 conv, stride 1, padding 1, + bias (DepthConv.depth_conv,
  * DCVC-DC/src/models/layers.py:143-144).  w: [9][C] fp32 (tap-major). */
 int dcvc_dwconv3x3(dcvc_tensor x, dcvc_tensor y, const float *w,

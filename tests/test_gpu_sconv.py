@@ -169,3 +169,36 @@ def test_fused_ffn_matches_fp64(c, H, W):
     torch.cuda.synchronize()
     assert y is not None and h.lib().dcvc_last_kernel().decode().startswith("sffn_kernel")
     assert rel_err(out.ch(4, c).nchw().cpu(), ref) < TOL
+
+
+@pytest.mark.parametrize("cin,cout,adapt,H,W", [(64, 48, True, 37, 53), (48, 32, True, 20, 33), (32, 64, True, 17, 16),
+                                                (64, 64, False, 9, 70), (48, 48, False, 8, 16), (32, 32, False, 25, 31)])
+def test_fused_depthconv_matches_fp64(cin, cout, adapt, H, W):
+    """sdc.hip: DepthConv (DCVC-DC/src/models/layers.py:135-163) = conv2(dw3x3(
+    lrelu(conv1(x) + b1, 0.01)) + bdw) + b2 + (adaptor(x) | x) in one kernel,
+    on channel views and image edges, against fp64."""
+    h = K()
+    g = torch.Generator().manual_seed(cin * 7 + cout + H)
+    big = torch.randn(1, cin + 8, H, W, generator=g)
+    x = big[:, 4:4 + cin]
+    w1 = torch.randn(cin, cin, 1, 1, generator=g) / cin ** 0.5
+    b1 = torch.randn(cin, generator=g) * 0.1
+    wd = torch.randn(cin, 1, 3, 3, generator=g) / 3
+    bd = torch.randn(cin, generator=g) * 0.1
+    w2 = torch.randn(cout, cin, 1, 1, generator=g) / cin ** 0.5
+    b2 = torch.randn(cout, generator=g) * 0.1
+    wa = torch.randn(cout, cin, 1, 1, generator=g) / cin ** 0.5 if adapt else None
+    ba = torch.randn(cout, generator=g) * 0.1 if adapt else None
+    xd = x.double()
+    t = F.leaky_relu(F.conv2d(xd, w1.double(), b1.double()), 0.01)
+    t = F.conv2d(t, wd.double(), bd.double(), padding=1, groups=cin)
+    idn = F.conv2d(xd, wa.double(), ba.double()) if adapt else xd
+    ref = F.conv2d(t, w2.double(), b2.double()) + idn
+    w9c = wd.reshape(cin, 9).t().contiguous()
+    dw = h.DcW(w1, b1, w9c, bd, w2, b2, wa, ba)
+    xa = h.from_nchw(big, h.F32).ch(4, cin)
+    out = h.empty(H, W, cout + 8, h.F32)
+    y = h.depth_conv_split(dw, xa, out.ch(8, cout), slope=0.01)
+    torch.cuda.synchronize()
+    assert y is not None and h.lib().dcvc_last_kernel().decode().startswith("sdc_kernel")
+    assert rel_err(out.ch(8, cout).nchw().cpu(), ref) < TOL
