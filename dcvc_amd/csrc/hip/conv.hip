@@ -580,6 +580,8 @@ extern "C" void dcvc_internal_sconv_occupancy(int v);
 extern "C" void dcvc_internal_sconv_waves(int v);
 extern "C" void dcvc_internal_sconv_resident(int v);
 extern "C" void dcvc_internal_sconv_res_waves(int v);
+extern "C" void dcvc_internal_sgemm_cfg(int v);
+extern "C" void dcvc_internal_sgemm_pd(int v);
 
 extern "C" int dcvc_conv2d(const dcvc_conv_args *a, void *stream) {
   if (!a || !a->w || !valid_view(a->x) || !valid_view(a->y)) return DCVC_HIP_EINVAL;
@@ -758,6 +760,14 @@ extern "C" int dcvc_set_option(const char *name, int value) {
   }
   if (std::strcmp(name, "sconv_res_waves") == 0) {
     dcvc_internal_sconv_res_waves(value);
+    return DCVC_HIP_OK;
+  }
+  if (std::strcmp(name, "sgemm_pd") == 0) {
+    dcvc_internal_sgemm_pd(value);
+    return DCVC_HIP_OK;
+  }
+  if (std::strcmp(name, "sgemm") == 0) {
+    dcvc_internal_sgemm_cfg(value);
     return DCVC_HIP_OK;
   }
   if (std::strcmp(name, "sconv_resident") == 0) {

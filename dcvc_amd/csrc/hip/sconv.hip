@@ -657,6 +657,7 @@ int pick_bn(SP p, hipStream_t st) {
 }  // namespace
 
 extern "C" void dcvc_internal_sconv_occupancy(int v) { g_occ = v; }
+extern "C" int dcvc_internal_sgemm(const dcvc_conv_args *a, void *stream);
 extern "C" void dcvc_internal_sconv_waves(int v) { g_waves = v; }
 extern "C" void dcvc_internal_sconv_resident(int v) { g_resident = v; }
 extern "C" void dcvc_internal_sconv_res_waves(int v) { g_res_waves = v; }
@@ -669,6 +670,10 @@ extern "C" int dcvc_internal_sconv(const dcvc_conv_args *a, void *stream) {
   if (a->kh != a->kw || (a->kh != 1 && a->kh != 3 && a->kh != 7)) return DCVC_HIP_EUNSUPPORTED;
   if (a->stride != 1 && !(a->stride == 2 && a->kh != 7)) return DCVC_HIP_EUNSUPPORTED;
   if (a->in_op == DCVC_IN_GATE && a->kh != 1) return DCVC_HIP_EUNSUPPORTED;
+  if (a->kh == 1) {   // the pixel-GEMM kernel (sgemm.hip) where it applies
+    const int r = dcvc_internal_sgemm(a, stream);
+    if (r != DCVC_HIP_EUNSUPPORTED) return r;
+  }
   SP p{};
   p.x = reinterpret_cast<const float *>(a->x.ptr);
   p.H = a->x.H;

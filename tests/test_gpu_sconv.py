@@ -77,9 +77,75 @@ def test_sconv_matches_fp64(case):
     cw = h.ConvW(w, b, s, h.F16X3)
     y = h.conv(cw, h.from_nchw(x, h.F32), out_dtype=h.F32)
     torch.cuda.synchronize()
-    assert h.lib().dcvc_last_kernel().decode().startswith("sconv_kernel")
+    kern = h.lib().dcvc_last_kernel().decode()
+    assert kern.startswith("sgemm_kernel" if k == 1 and s == 1 and cin % 8 == 0 else "sconv_kernel"), kern
     err = rel_err(y.nchw().cpu(), ref)
     assert err < TOL, (case, err)
+
+
+# the 1x1 pixel-GEMM kernel (sgemm.hip) in each forced (BN, pixel groups)
+# configuration: latent sizes, ragged pixel counts, output channels that pad
+# the n-block, in_op lrelu and the whole epilogue on channel views
+SGEMM_CFGS = {1: (128, 2), 2: (64, 2), 3: (32, 2), 4: (128, 1), 5: (64, 1), 6: (32, 1)}
+
+
+@pytest.mark.parametrize("cfg", sorted(SGEMM_CFGS))
+@pytest.mark.parametrize("cin,cout,H,W", [(1024, 384, 68, 120), (384, 1024, 17, 23), (192, 48, 9, 7),
+                                          (40, 36, 5, 31), (8, 4, 3, 3)])
+def test_sgemm_matches_fp64(cfg, cin, cout, H, W):
+    h = K()
+    g = torch.Generator().manual_seed(cin + cout + cfg)
+    x = torch.randn(1, cin, H, W, generator=g)
+    x[:, ::5] *= 1e-3
+    w = torch.randn(cout, cin, 1, 1, generator=g) / cin ** 0.5
+    b = torch.randn(cout, generator=g) * 0.1
+    ref = F.conv2d(x.double(), w.double(), b.double())
+    cw = h.ConvW(w, b, 1, h.F16X3)
+    h.set_option("sgemm", cfg)
+    try:
+        y = h.conv(cw, h.from_nchw(x, h.F32), out_dtype=h.F32)
+        torch.cuda.synchronize()
+        bn, pxw = SGEMM_CFGS[cfg]
+        assert h.lib().dcvc_last_kernel().decode() == f"sgemm_kernel<{bn}, {pxw}, 3>"
+    finally:
+        h.set_option("sgemm", 0)
+    err = rel_err(y.nchw().cpu(), ref)
+    assert err < TOL, err
+
+
+@pytest.mark.parametrize("cfg", [0, 2, 6])
+def test_sgemm_epilogue_and_views(cfg):
+    h = K()
+    cin, cout, H, W = 96, 40, 13, 29
+    g = torch.Generator().manual_seed(11)
+    big = torch.randn(1, cin + 8, H, W, generator=g)
+    x = big[:, 4:4 + cin]
+    w = torch.randn(cout, cin, 1, 1, generator=g) / cin ** 0.5
+    b = torch.randn(cout, generator=g) * 0.1
+    r = torch.randn(1, cout, H, W, generator=g)
+    r2 = torch.randn(1, cout, H, W, generator=g)
+    sc = torch.rand(cout, generator=g) + 0.5
+    xd = F.leaky_relu(x.double(), 0.2)
+    ref = (r2.double() + (r.double() + F.leaky_relu(F.conv2d(xd, w.double(), b.double()), 0.1))) \
+        * sc.double().view(1, -1, 1, 1)
+    cw = h.ConvW(w, b, 1, h.F16X3)
+    xa = h.from_nchw(big, h.F32).ch(4, cin)
+    out = h.empty(H, W, cout + 12, h.F32)
+    out.buf.fill_(7.0)
+    ra = h.empty(H, W, cout + 4, h.F32)
+    h.copy(h.from_nchw(r, h.F32), ra.ch(4, cout))
+    r2a = h.from_nchw(r2, h.F32)
+    h.set_option("sgemm", cfg)
+    try:
+        h.conv(cw, xa, out.ch(8, cout), in_op=h.IN_LRELU, in_slope=0.2, act=h.ACT_LRELU, slope=0.1,
+               res=ra.ch(4, cout), res2=r2a, scale=sc.cuda())
+        torch.cuda.synchronize()
+        assert h.lib().dcvc_last_kernel().decode().startswith("sgemm_kernel")
+    finally:
+        h.set_option("sgemm", 0)
+    assert rel_err(out.ch(8, cout).nchw().cpu(), ref) < TOL
+    # the channels around the view are untouched
+    assert bool((out.buf[:, :, :8] == 7.0).all()) and bool((out.buf[:, :, 8 + cout:] == 7.0).all())
 
 
 def test_sconv_fused_epilogue_and_views():
