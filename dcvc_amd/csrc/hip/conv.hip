@@ -582,6 +582,7 @@ extern "C" void dcvc_internal_sconv_resident(int v);
 extern "C" void dcvc_internal_sconv_res_waves(int v);
 extern "C" void dcvc_internal_sgemm_cfg(int v);
 extern "C" void dcvc_internal_sgemm_pd(int v);
+extern "C" int dcvc_internal_set_option_split(const char *name, int value);
 
 extern "C" int dcvc_conv2d(const dcvc_conv_args *a, void *stream) {
   if (!a || !a->w || !valid_view(a->x) || !valid_view(a->y)) return DCVC_HIP_EINVAL;
@@ -786,5 +787,5 @@ extern "C" int dcvc_set_option(const char *name, int value) {
     dcvc_internal_conv3p_rows4(value);
     return DCVC_HIP_OK;
   }
-  return DCVC_HIP_EINVAL;
+  return dcvc_internal_set_option_split(name, value);   // the split-precision kernels' options (sconvr.hip)
 }

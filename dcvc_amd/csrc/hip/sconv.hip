@@ -76,6 +76,8 @@ struct SP {
   int nchunks, tpk_last;   // taps per K step of the last chunk (1, 2 or 4)
   int64_t wchunk;          // halves of one full chunk's packed weights (hi + lo)
   int wbytes;              // bytes of the packed weights
+  int dbg;                 // dcvc_set_option("sconv_dbg", mask): timing ablations, wrong results
+                           // (1 no MFMA, 2 no image publish, 4 no image loads, 8 no epilogue)
 };
 
 // RES = false: weights streamed one kernel row (KS taps) of one chunk per
@@ -437,7 +439,7 @@ __global__ void __launch_bounds__(NW * 64) sconv_kernel(SP p) {
       int c, r0, tpk;
       stage_of(s, c, r0, tpk);
       if (r0 == 0) {
-        publish_img();   // waits for its own image loads
+        if (!(p.dbg & 2)) publish_img();   // waits for its own image loads
         if (s == 0) epi::stage_consts(p, Lc, n0, BN);
         wait_lgkm();
         raw_barrier();
@@ -447,11 +449,13 @@ __global__ void __launch_bounds__(NW * 64) sconv_kernel(SP p) {
         else if (more) issue_w(t + G, 0, (k + 1) & 1);
       }
       if (r0 == 0) {
-        if (c + 1 < p.nchunks) prefetch_img(t, c + 1), img_inflight = true;
+        if (p.dbg & 4) {
+        } else if (c + 1 < p.nchunks) prefetch_img(t, c + 1), img_inflight = true;
         else if (more) prefetch_img(t + G, 0), img_inflight = true;
       }
-      compute(s, k & 1);
+      if (!(p.dbg & 1)) compute(s, k & 1);
     }
+    if (p.dbg & 8) continue;
     if (p.direct) {
       // epilogue straight from the accumulators: lane (col, hi) of fragment
       // (r, j) holds output channels n0 + 16 j + 4 hi .. + 3 of pixel (row
@@ -531,6 +535,7 @@ __global__ void __launch_bounds__(NW * 64) sconv_kernel(SP p) {
 }
 
 int g_cus = 0;
+int g_dbg = 0;
 int g_occ = 0;   // dcvc_set_option("sconv_occupancy", n): workgroups per CU (0 = as many as the LDS holds)
 
 template <int KS, int S, int BN, int RW, int NW, bool GATE, bool RES>
@@ -567,6 +572,7 @@ int launch(SP p, hipStream_t st) {
   dcvc_note_kernel("sconv_kernel<%d, %d, %d, %d, %d, %s, %s>@%lld", KS, S, BN, RW, NW, bname(GATE), bname(RES),
                    (long long)G * kNT);
   dcvc_ensure_lds(reinterpret_cast<const void *>(kern), 160 * 1024);
+  p.dbg = g_dbg;
   hipLaunchKernelGGL(kern, dim3((unsigned)G), dim3(kNT), lds, st, p);
   DCVC_LAUNCH_CHECK();
   return DCVC_HIP_OK;
@@ -657,7 +663,9 @@ int pick_bn(SP p, hipStream_t st) {
 }  // namespace
 
 extern "C" void dcvc_internal_sconv_occupancy(int v) { g_occ = v; }
+extern "C" void dcvc_internal_sconv_dbg(int v) { g_dbg = v; }
 extern "C" int dcvc_internal_sgemm(const dcvc_conv_args *a, void *stream);
+extern "C" int dcvc_internal_sconvr(const dcvc_conv_args *a, void *stream);
 extern "C" void dcvc_internal_sconv_waves(int v) { g_waves = v; }
 extern "C" void dcvc_internal_sconv_resident(int v) { g_resident = v; }
 extern "C" void dcvc_internal_sconv_res_waves(int v) { g_res_waves = v; }
@@ -672,6 +680,10 @@ extern "C" int dcvc_internal_sconv(const dcvc_conv_args *a, void *stream) {
   if (a->in_op == DCVC_IN_GATE && a->kh != 1) return DCVC_HIP_EUNSUPPORTED;
   if (a->kh == 1) {   // the pixel-GEMM kernel (sgemm.hip) where it applies
     const int r = dcvc_internal_sgemm(a, stream);
+    if (r != DCVC_HIP_EUNSUPPORTED) return r;
+  }
+  if (a->kh == 3 && a->stride == 1) {   // the register-image kernel (sconvr.hip) where it applies
+    const int r = dcvc_internal_sconvr(a, stream);
     if (r != DCVC_HIP_EUNSUPPORTED) return r;
   }
   SP p{};
