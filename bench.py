@@ -155,21 +155,30 @@ def shard_seed(rank):
 
 
 def host_info():
-    """nproc, the cores this process may run on, and the CPU model."""
+    """nproc, the cores this process may run on, the physical cores of the
+    node (distinct (physical id, core id) pairs) and the CPU model."""
     model = "unknown"
+    cores, phys, core = set(), None, None
     try:
         with open("/proc/cpuinfo") as f:
             for line in f:
-                if line.startswith("model name"):
+                if line.startswith("model name") and model == "unknown":
                     model = line.split(":", 1)[1].strip()
-                    break
+                elif line.startswith("physical id"):
+                    phys = line.split(":", 1)[1].strip()
+                elif line.startswith("core id"):
+                    core = line.split(":", 1)[1].strip()
+                elif not line.strip():
+                    if core is not None:
+                        cores.add((phys, core))
+                    phys, core = None, None
     except OSError:
         pass
     try:
         usable = len(os.sched_getaffinity(0))
     except AttributeError:
         usable = os.cpu_count() or 1
-    return {"nproc": os.cpu_count() or 1, "usable": usable, "cpu": model}
+    return {"nproc": os.cpu_count() or 1, "usable": usable, "physical_cores": len(cores) or None, "cpu": model}
 
 
 def oracle_ip_times(isd, psd, args, threads, capture=None):
@@ -266,7 +275,17 @@ def _workers_record(args):
             rec = json.load(f)
     except (OSError, ValueError):
         return None
-    return rec if rec.get("workload") == [args.model, args.height, args.width, bool(args.yuv420)] else None
+    if rec.get("workload") != [args.model, args.height, args.width, bool(args.yuv420)]:
+        return None
+    # the record's rate per worker core and, for scale, that rate times this
+    # node's physical cores (linear scaling assumed: an upper bound, the
+    # workers share memory bandwidth)
+    rec["per_core_fps"] = rec["value"] / rec["cores"]
+    pc = host_info()["physical_cores"]
+    if pc:
+        rec["node_physical_cores"] = pc
+        rec["node_total_fps_est"] = rec["per_core_fps"] * pc
+    return rec
 
 
 def _worker(job):
