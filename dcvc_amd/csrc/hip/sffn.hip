@@ -310,12 +310,18 @@ int hs_of(int c) { return c >= 128 ? 32 : 64; }
 
 }  // namespace
 
+extern "C" int dcvc_internal_lffn_supported(int c, int hidden);
+extern "C" int64_t dcvc_internal_lffn_pack(const float *w1, const float *w2, int c, int hidden, void *out);
+extern "C" int dcvc_internal_lffn(const dcvc_ffn_args *a, void *stream);
+
 // Packed slices of one ConvFFN: w1 [hidden][c] (conv.0, fp32 host), w2
 // [c][hidden] (conv.2); each slice of HS hidden channels is the LDS image
 // sffn_kernel reads (hi and lo of ffn1 as [kc][h][32], then of ffn2 as
 // [kc2][n][32], 16-byte slots swizzled by swz()).  out NULL: size query.
 extern "C" int64_t dcvc_ffn_pack_weights(const float *w1, const float *w2, int c, int hidden, void *out) {
   if (!w1 || !w2 || c <= 0 || hidden <= 0) return DCVC_HIP_EINVAL;
+  // the latent widths: MFMA fragments for slffn.hip
+  if (dcvc_internal_lffn_supported(c, hidden)) return dcvc_internal_lffn_pack(w1, w2, c, hidden, out);
   const int HS = hs_of(c);
   if (hidden % HS) return DCVC_HIP_EINVAL;
   const int kc1 = (c + 31) / 32, c16 = (c + 15) / 16 * 16, kc2 = HS / 32;
@@ -359,6 +365,7 @@ extern "C" int dcvc_conv_ffn(const dcvc_ffn_args *a, void *stream) {
   if (a->x.cstride % 4 || a->x.coff % 4 || a->y.cstride % 4 || a->y.coff % 4 || a->c % 8 ||
       ((uintptr_t)a->x.ptr & 15) || ((uintptr_t)a->y.ptr & 15))
     return DCVC_HIP_EUNSUPPORTED;
+  if (dcvc_internal_lffn_supported(a->c, a->hidden)) return dcvc_internal_lffn(a, stream);   // slffn.hip
   FP p{};
   p.x = reinterpret_cast<const float *>(a->x.ptr);
   p.npix = a->x.H * a->x.W;

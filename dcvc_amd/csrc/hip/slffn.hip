@@ -1,0 +1,316 @@
+// Fused ConvFFN of the latent DepthConvBlocks in split-fp16 arithmetic:
+//   out = scale * (x + lrelu(ffn2(lrelu(ffn1(x) + b1)) + b2))
+// DCVC-DC/src/models/layers.py:166-179 (ConvFFN, hidden = max(min(4C, 1024),
+// 2C)) as the entropy model's prior fusion and spatial prior stacks run it on
+// the 1/16 latent (video_model.py:288-305: C = 384, hidden 1024; the motion
+// branch :250-267: C = 192, hidden 768).
+//
+// Why a kernel of its own: at 1080p the latent is 68 x 120 = 8160 pixels, so
+// each of the two unfused 1x1 GEMMs (sgemm.hip) has only ~250 pixel x channel
+// tiles, walks K = 384..1024 serially and pays a launch, a grid ramp and an
+// epilogue, while the 4C-wide hidden map makes an fp32 round trip through
+// memory: ~95 us per 384-channel FFN for ~13 GFLOP of f16x3 work.  Here one
+// workgroup owns 32 pixels and ALL channels of the block:
+//   * the tile's input (C fp32 channels) is split once into (hi, lo) fp16
+//     LDS images (sconv.hip's split and swizzle);
+//   * the hidden layer goes in slices of 64 channels: wave w computes hidden
+//     rows [16 w, 16 w + 16) of the slice for the 32 pixels (K = C), adds
+//     b1, applies the LeakyReLU in fp32, splits the result into a hidden LDS
+//     image (two buffers: one barrier per slice), and every wave then
+//     accumulates its C / 4 output rows over the slice (ffn2, K = 64);
+//   * no LDS staging of weights: they are packed as MFMA A fragments (1 KiB
+//     per 16 rows x 32 K, lane-ordered, hi and lo planes) and loaded straight
+//     into registers, ffn1's of slice s + 1 during ffn2 of slice s and
+//     ffn2's of slice s during ffn1 of slice s; every weight byte crosses
+//     the L2 once per workgroup;
+//   * the epilogue runs from the accumulators: + b2, LeakyReLU, + x (fp32,
+//     re-read from L2), * scale, 16-byte stores.
+// The products and the K order of both GEMMs are those of sgemm.hip (chunks
+// of 32 ascending, main and correction accumulators), so the block's output
+// is bit-identical to the two unfused launches.
+#include "common.h"
+#include "split.h"
+
+#include <cstring>
+
+namespace {
+
+constexpr int kNW = 4, kNT = kNW * 64;
+constexpr int P = 32;     // pixels per workgroup (two 16-pixel MFMA column blocks)
+constexpr int HS = 64;    // hidden channels per slice (4 row blocks: one per wave)
+constexpr int kOob = 0x7fffffe0;
+
+struct LP {
+  const float *x;
+  int npix, xcs, xco, xbytes;
+  float *y;
+  int ycs, yco, ybytes;
+  const uint16_t *w1, *w2;   // packed fragments (dcvc_internal_lffn_pack)
+  int w1bytes, w2bytes;
+  const float *b1, *b2, *scale;
+  int hidden;
+  float slope;
+};
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void *base, int bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), (short)0, bytes, 0x00020000);
+}
+
+template <int C>
+__global__ void __launch_bounds__(kNT) slffn_kernel(LP p) {
+  constexpr int KC = C / 32;        // ffn1 K chunks
+  constexpr int NTW = C / 64;       // ffn2 output row blocks per wave
+  constexpr int XI = KC * P * 32;   // halves of the input image (hi or lo)
+  constexpr int HI = 2 * P * 32;    // halves of one hidden image (hi or lo): 2 chunks of 32
+  extern __shared__ __align__(16) unsigned char smem[];
+  uint16_t *Xh = reinterpret_cast<uint16_t *>(smem), *Xl = Xh + XI;
+  uint16_t *Hb = Xl + XI;           // [buf][hi, lo][HI]
+  float *Lb1 = reinterpret_cast<float *>(Hb + 4 * HI);
+  float *Lb2 = Lb1 + p.hidden, *Lsc = Lb2 + C;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int col = lane & 15, g = lane >> 4;
+  const int pix0 = blockIdx.x * P;
+  const int KH = p.hidden / 32;     // ffn2 K chunks over the whole hidden layer
+  const int nsl = p.hidden / HS;
+
+  const __amdgpu_buffer_rsrc_t xr = rsrc(p.x + p.xco, p.xbytes);
+  const __amdgpu_buffer_rsrc_t w1r = rsrc(p.w1, p.w1bytes);
+  const __amdgpu_buffer_rsrc_t w2r = rsrc(p.w2, p.w2bytes);
+
+  // fragment f of a packed matrix: lane's 8 halves of the hi plane at f *
+  // 1024 + lane * 8, of the lo plane 512 halves further
+  auto ldfrag = [&](const __amdgpu_buffer_rsrc_t &r, int f, f16x8 &h, f16x8 &l) {
+    const int o = (f * 1024 + lane * 8) * 2;
+    h = __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(r, o, 0, 0));
+    l = __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(r, o + 1024, 0, 0));
+  };
+
+  // ffn1 fragments of slice 0 first: their latency hides behind the image
+  f16x8 a1h[KC], a1l[KC];
+#pragma unroll
+  for (int kc = 0; kc < KC; ++kc) ldfrag(w1r, wave * KC + kc, a1h[kc], a1l[kc]);
+
+  // input image: piece u = (pixel, 8-channel group), split once
+  {
+    constexpr int NPC = P * C / 8;
+#pragma unroll
+    for (int u = tid; u < NPC; u += kNT) {
+      const int px = u / (C / 8), c8 = u - px * (C / 8);
+      const bool ok = pix0 + px < p.npix;
+      const int o = ok ? ((pix0 + px) * p.xcs + c8 * 8) * 4 : kOob;
+      const f32x4 a = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, o, 0, 0));
+      const f32x4 b = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, o + 16, 0, 0));
+      const float v[8] = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+      u32x4_t h, l;
+      split8(v, h, l);
+      const int off = swz((c8 >> 2) * P + px, c8 & 3);
+      *reinterpret_cast<u32x4_t *>(Xh + off) = h;
+      *reinterpret_cast<u32x4_t *>(Xl + off) = l;
+    }
+    for (int i = tid; i < p.hidden; i += kNT) Lb1[i] = p.b1[i];
+    for (int i = tid; i < C; i += kNT) {
+      Lb2[i] = p.b2[i];
+      Lsc[i] = p.scale ? p.scale[i] : 1.f;
+    }
+  }
+  __syncthreads();
+
+  f32x4 om[NTW][2], oc[NTW][2];
+#pragma unroll
+  for (int j = 0; j < NTW; ++j)
+#pragma unroll
+    for (int pb = 0; pb < 2; ++pb) {
+      om[j][pb] = f32x4{0.f, 0.f, 0.f, 0.f};
+      oc[j][pb] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  const float slope = p.slope;
+
+  for (int s = 0; s < nsl; ++s) {
+    // ffn2 fragments of this slice: rows (wave * NTW + j) * 16, K chunks 2 s, 2 s + 1
+    f16x8 a2h[NTW][2], a2l[NTW][2];
+#pragma unroll
+    for (int j = 0; j < NTW; ++j)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) ldfrag(w2r, (wave * NTW + j) * KH + 2 * s + kk, a2h[j][kk], a2l[j][kk]);
+
+    // ffn1: hidden rows s * 64 + 16 wave .. + 15 for both pixel blocks
+    f32x4 hm[2], hc[2];
+#pragma unroll
+    for (int pb = 0; pb < 2; ++pb) {
+      hm[pb] = f32x4{0.f, 0.f, 0.f, 0.f};
+      hc[pb] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int kc = 0; kc < KC; ++kc)
+#pragma unroll
+      for (int pb = 0; pb < 2; ++pb) {
+        const int o = swz(kc * P + pb * 16 + col, g);
+        const f16x8 bh = *reinterpret_cast<const f16x8 *>(Xh + o);
+        const f16x8 bl = *reinterpret_cast<const f16x8 *>(Xl + o);
+        hm[pb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1h[kc], bh, hm[pb], 0, 0, 0);
+        hc[pb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1h[kc], bl, hc[pb], 0, 0, 0);
+        hc[pb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1l[kc], bh, hc[pb], 0, 0, 0);
+      }
+    // the next slice's ffn1 fragments (the registers are free now)
+    if (s + 1 < nsl) {
+#pragma unroll
+      for (int kc = 0; kc < KC; ++kc) ldfrag(w1r, ((s + 1) * 4 + wave) * KC + kc, a1h[kc], a1l[kc]);
+    }
+    // hidden = lrelu(acc + b1) in fp32, split into this slice's hidden image:
+    // lane (col, g) holds hidden channels 16 wave + 4 g .. + 3 of pixel
+    // pb * 16 + col: chunk wave >> 1, slot (wave & 1) * 2 + (g >> 1), halves
+    // (g & 1) * 4 .. + 3 of the slot
+    uint16_t *Hh = Hb + (s & 1) * 2 * HI, *Hl = Hh + HI;
+#pragma unroll
+    for (int pb = 0; pb < 2; ++pb) {
+      float v[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float t = (hm[pb][e] + hc[pb][e] * kLoInv) + Lb1[s * HS + wave * 16 + g * 4 + e];
+        v[e] = t >= 0.f ? t : t * slope;
+      }
+      const auto h0 = __builtin_amdgcn_cvt_pkrtz(v[0], v[1]);
+      const auto h1 = __builtin_amdgcn_cvt_pkrtz(v[2], v[3]);
+      const uint32_t l0 = pk((v[0] - (float)h0[0]) * 2048.f, (v[1] - (float)h0[1]) * 2048.f);
+      const uint32_t l1 = pk((v[2] - (float)h1[0]) * 2048.f, (v[3] - (float)h1[1]) * 2048.f);
+      const int off = swz((wave >> 1) * P + pb * 16 + col, (wave & 1) * 2 + (g >> 1)) + (g & 1) * 4;
+      typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
+      *reinterpret_cast<u32x2_t *>(Hh + off) =
+          u32x2_t{__builtin_bit_cast(uint32_t, h0), __builtin_bit_cast(uint32_t, h1)};
+      *reinterpret_cast<u32x2_t *>(Hl + off) = u32x2_t{l0, l1};
+    }
+    // every wave's hidden rows of slice s are in; (every wave finished ffn2
+    // of slice s - 1 before it got here, so buffer (s + 1) & 1 is free next)
+    __syncthreads();
+    // ffn2 over the slice: K chunks 2 s, 2 s + 1 of the hidden layer
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int pb = 0; pb < 2; ++pb) {
+        const int o = swz(kk * P + pb * 16 + col, g);
+        const f16x8 bh = *reinterpret_cast<const f16x8 *>(Hh + o);
+        const f16x8 bl = *reinterpret_cast<const f16x8 *>(Hl + o);
+#pragma unroll
+        for (int j = 0; j < NTW; ++j) {
+          om[j][pb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a2h[j][kk], bh, om[j][pb], 0, 0, 0);
+          oc[j][pb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a2h[j][kk], bl, oc[j][pb], 0, 0, 0);
+          oc[j][pb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a2l[j][kk], bh, oc[j][pb], 0, 0, 0);
+        }
+      }
+  }
+
+  // epilogue: lane (col, g) of fragment (j, pb) holds output channels
+  // (wave * NTW + j) * 16 + 4 g .. + 3 of pixel pix0 + pb * 16 + col
+  const __amdgpu_buffer_rsrc_t yr = rsrc(p.y + p.yco, p.ybytes);
+#pragma unroll
+  for (int pb = 0; pb < 2; ++pb) {
+    const int px = pix0 + pb * 16 + col;
+    const bool ok = px < p.npix;
+    f32x4 xv[NTW];
+#pragma unroll
+    for (int j = 0; j < NTW; ++j) {
+      const int n = (wave * NTW + j) * 16 + 4 * g;
+      xv[j] = __builtin_bit_cast(f32x4,
+                                 __builtin_amdgcn_raw_buffer_load_b128(xr, ok ? (px * p.xcs + n) * 4 : kOob, 0, 0));
+    }
+#pragma unroll
+    for (int j = 0; j < NTW; ++j) {
+      const int n = (wave * NTW + j) * 16 + 4 * g;
+      f32x4 v;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float t = (om[j][pb][e] + oc[j][pb][e] * kLoInv) + Lb2[n + e];
+        t = t >= 0.f ? t : t * slope;
+        t = xv[j][e] + t;
+        v[e] = t * Lsc[n + e];
+      }
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, v), yr, ok ? (px * p.ycs + n) * 4 : kOob, 0,
+                                             0);
+    }
+  }
+}
+
+template <int C>
+int run(LP p, hipStream_t st) {
+  constexpr int KC = C / 32;
+  const size_t lds = (size_t)2 * KC * P * 32 * 2 + (size_t)4 * 2 * P * 32 * 2 + (size_t)(p.hidden + 2 * C) * 4;
+  if (lds > 160 * 1024) return DCVC_HIP_EUNSUPPORTED;
+  const int G = (p.npix + P - 1) / P;
+  auto kern = slffn_kernel<C>;
+  dcvc_note_kernel("slffn_kernel<%d>@%lld", C, (long long)G * kNT);
+  dcvc_ensure_lds(reinterpret_cast<const void *>(kern), 160 * 1024);
+  hipLaunchKernelGGL(kern, dim3((unsigned)G), dim3(kNT), lds, st, p);
+  DCVC_LAUNCH_CHECK();
+  return DCVC_HIP_OK;
+}
+
+// packed fragments of an R x K matrix (R multiple of 16, K of 32): fragment
+// (rb, kc) = rows [16 rb, 16 rb + 16) x K [32 kc, 32 kc + 32), index rb *
+// (K / 32) + kc, 1024 halves: hi plane then lo plane, each lane-ordered --
+// lane (i, kg) = kg * 16 + i holds row 16 rb + i, K 32 kc + 8 kg .. + 7
+void pack_frags(const float *m, int R, int K, uint16_t *o) {
+  const int kcs = K / 32;
+  for (int rb = 0; rb < R / 16; ++rb)
+    for (int kc = 0; kc < kcs; ++kc) {
+      uint16_t *f = o + ((int64_t)rb * kcs + kc) * 1024;
+      for (int lane = 0; lane < 64; ++lane) {
+        const int i = lane & 15, kg = lane >> 4;
+        for (int e = 0; e < 8; ++e) {
+          const float v = m[(int64_t)(rb * 16 + i) * K + kc * 32 + kg * 8 + e];
+          host_split(v, f[lane * 8 + e], f[512 + lane * 8 + e]);
+        }
+      }
+    }
+}
+
+}  // namespace
+
+// the latent widths this kernel takes (C = 192, 384; hidden a multiple of 64)
+extern "C" int dcvc_internal_lffn_supported(int c, int hidden) {
+  return (c == 192 || c == 384) && hidden > 0 && hidden % HS == 0;
+}
+
+// w1 [hidden][c] (conv.0), w2 [c][hidden] (conv.2) as packed fragments: ffn1's
+// (hidden / 16 x c / 32 fragments) then ffn2's (c / 16 x hidden / 32).
+extern "C" int64_t dcvc_internal_lffn_pack(const float *w1, const float *w2, int c, int hidden, void *out) {
+  if (!dcvc_internal_lffn_supported(c, hidden)) return DCVC_HIP_EINVAL;
+  const int64_t n1 = (int64_t)hidden * c * 2, n2 = (int64_t)c * hidden * 2;
+  if (!out) return n1 + n2;
+  uint16_t *o = reinterpret_cast<uint16_t *>(out);
+  pack_frags(w1, hidden, c, o);
+  pack_frags(w2, c, hidden, o + n1);
+  return n1 + n2;
+}
+
+extern "C" int dcvc_internal_lffn(const dcvc_ffn_args *a, void *stream) {
+  if (!dcvc_internal_lffn_supported(a->c, a->hidden)) return DCVC_HIP_EUNSUPPORTED;
+  const int64_t npix = (int64_t)a->x.H * a->x.W;
+  if (npix <= 0) return DCVC_HIP_OK;
+  auto bytes = [&](int cs, int co) { return (npix * cs - co) * 4; };
+  if (bytes(a->x.cstride, a->x.coff) > 0x7fff0000 || bytes(a->y.cstride, a->y.coff) > 0x7fff0000)
+    return DCVC_HIP_EUNSUPPORTED;
+  LP p{};
+  p.x = reinterpret_cast<const float *>(a->x.ptr);
+  p.npix = (int)npix;
+  p.xcs = a->x.cstride;
+  p.xco = a->x.coff;
+  p.xbytes = (int)bytes(a->x.cstride, a->x.coff);
+  p.y = reinterpret_cast<float *>(a->y.ptr);
+  p.ycs = a->y.cstride;
+  p.yco = a->y.coff;
+  p.ybytes = (int)bytes(a->y.cstride, a->y.coff);
+  const int64_t n1 = (int64_t)a->hidden * a->c * 2;
+  p.w1 = reinterpret_cast<const uint16_t *>(a->w);
+  p.w2 = p.w1 + n1;
+  p.w1bytes = (int)(n1 * 2);
+  p.w2bytes = (int)(n1 * 2);
+  p.b1 = a->b1;
+  p.b2 = a->b2;
+  p.scale = a->scale;
+  p.hidden = a->hidden;
+  p.slope = a->slope;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  return a->c == 384 ? run<384>(p, st) : run<192>(p, st);
+}

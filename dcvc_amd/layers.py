@@ -164,8 +164,10 @@ class DepthConvBlock:
                              sd[d + ".adaptor.weight"] if self.adaptor is not None else None,
                              sd[d + ".adaptor.bias"] if self.adaptor is not None else None, ctx.dev)
         self.ffn = None
-        if (FUSE_FFN and not gated and self.ffn2.compute == F16X3 and self.cout in (32, 48, 64, 128)
-                and self.ffn1.cout % (32 if self.cout >= 128 else 64) == 0):
+        # (sffn.hip for the feature-rate widths; slffn.hip for the latent
+        # 192 / 384-channel blocks of the entropy model)
+        if (FUSE_FFN and not gated and self.ffn2.compute == F16X3 and self.cout in (32, 48, 64, 128, 192, 384)
+                and self.ffn1.cout % (64 if self.cout != 128 else 32) == 0):
             sd = ctx.sd
             self.ffn = K.FfnW(sd[f + ".conv.0.weight"], sd[f + ".conv.0.bias"], sd[f + ".conv.2.weight"],
                               sd[f + ".conv.2.bias"], ctx.dev)

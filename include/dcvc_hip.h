@@ -140,8 +140,11 @@ int dcvc_depthconv_block(const dcvc_dcb_args *a, void *stream);
  * DCVC-DC/src/models/layers.py:166-179 with the DepthConvBlock's optional
  * output scale:  y = scale * (x + lrelu(ffn2(lrelu(ffn1(x) + b1)) + b2)),
  * lrelu slope `slope` (0.1), fp32 views of c channels (c in {32, 48, 64, 128},
- * hidden a multiple of 64, or of 32 for c = 128); the hidden layer never
- * leaves LDS.  Weights packed by dcvc_ffn_pack_weights from w1 = conv.0
+ * hidden a multiple of 64, or of 32 for c = 128; and the entropy model's
+ * latent widths c in {192, 384}, hidden a multiple of 64, whose weights are
+ * packed as MFMA fragments streamed from L2, DCVC-DC/src/models/
+ * video_model.py:250-305); the hidden layer never leaves the CU.
+ * Weights packed by dcvc_ffn_pack_weights from w1 = conv.0
  * [hidden][c] and w2 = conv.2 [c][hidden] (fp32, host); out NULL returns the
  * element count.  DCVC_HIP_EUNSUPPORTED for other shapes (the caller runs
  * the two convs).

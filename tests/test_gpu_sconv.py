@@ -313,6 +313,43 @@ def test_fused_ffn_matches_fp64(c, H, W):
     assert rel_err(out.ch(4, c).nchw().cpu(), ref) < TOL
 
 
+@pytest.mark.parametrize("c,H,W", [(384, 68, 120), (192, 68, 120), (384, 17, 30), (192, 5, 7), (384, 3, 11)])
+def test_latent_ffn_matches_fp64_and_unfused(c, H, W):
+    """slffn.hip: the latent ConvFFN (C = 384 / 192, hidden = max(min(4C,
+    1024), 2C), DCVC-DC/src/models/layers.py:166-179) in one kernel on a
+    channel view, against fp64, and bit-identical to the two unfused
+    split-fp16 GEMM launches (same products, same K order); 68 x 120 is the
+    1080p latent, the others ragged 32-pixel tiles."""
+    h = K()
+    g = torch.Generator().manual_seed(c + H * W)
+    hid = max(min(4 * c, 1024), 2 * c)
+    big = torch.randn(1, c + 8, H, W, generator=g)
+    x = big[:, 4:4 + c]
+    w1 = torch.randn(hid, c, 1, 1, generator=g) / c ** 0.5
+    b1 = torch.randn(hid, generator=g) * 0.1
+    w2 = torch.randn(c, hid, 1, 1, generator=g) / hid ** 0.5
+    b2 = torch.randn(c, generator=g) * 0.1
+    sc = torch.rand(c, generator=g) + 0.5
+    xd = x.double()
+    hh = F.leaky_relu(F.conv2d(xd, w1.double(), b1.double()), 0.1)
+    ref = (xd + F.leaky_relu(F.conv2d(hh, w2.double(), b2.double()), 0.1)) * sc.double().view(1, -1, 1, 1)
+    fw = h.FfnW(w1, b1, w2, b2)
+    xa = h.from_nchw(big, h.F32).ch(4, c)
+    out = h.empty(H, W, c + 8, h.F32)
+    out.buf.fill_(7.0)
+    y = h.conv_ffn(fw, xa, out.ch(4, c), scale=sc.cuda(), slope=0.1)
+    torch.cuda.synchronize()
+    assert y is not None and h.lib().dcvc_last_kernel().decode().startswith("slffn_kernel")
+    got = out.ch(4, c).nchw().cpu()
+    assert rel_err(got, ref) < TOL
+    assert bool((out.buf[:, :, :4] == 7.0).all()) and bool((out.buf[:, :, 4 + c:] == 7.0).all())
+    c1, c2 = h.ConvW(w1, b1, 1, h.F16X3), h.ConvW(w2, b2, 1, h.F16X3)
+    t = h.conv(c1, xa, act=h.ACT_LRELU, slope=0.1)
+    y2 = h.conv(c2, t, act=h.ACT_LRELU, slope=0.1, res=xa, scale=sc.cuda())
+    torch.cuda.synchronize()
+    assert torch.equal(y2.nchw().cpu(), got)
+
+
 @pytest.mark.parametrize("cin,cout,adapt,H,W", [(64, 48, True, 37, 53), (48, 32, True, 20, 33), (32, 64, True, 17, 16),
                                                 (64, 64, False, 9, 70), (48, 48, False, 8, 16), (32, 32, False, 25, 31)])
 def test_fused_depthconv_matches_fp64(cin, cout, adapt, H, W):
