@@ -1,3 +1,6 @@
+// Fused latent DepthConvBlock stages in split-fp16 arithmetic (slffn_kernel:
+// the ConvFFN; sldc_kernel below: the DepthConv tail).
+//
 // Fused ConvFFN of the latent DepthConvBlocks in split-fp16 arithmetic:
 //   out = scale * (x + lrelu(ffn2(lrelu(ffn1(x) + b1)) + b2))
 // DCVC-DC/src/models/layers.py:166-179 (ConvFFN, hidden = max(min(4C, 1024),
@@ -232,6 +235,172 @@ __global__ void __launch_bounds__(kNT) slffn_kernel(LP p) {
   }
 }
 
+// The tail of a latent DepthConv (DCVC-DC/src/models/layers.py:135-163,
+// adaptor-free blocks C -> C of the entropy model, video_model.py:250-305):
+//   out = conv2(dw3x3(t) + bdw) + b2 + x
+// with t = lrelu(conv1(x) + b1) from the previous launch.  Unfused this is a
+// depthwise launch (an fp32 round trip of the C-channel map) and a 1x1 GEMM
+// launch on 8160 pixels.  One workgroup owns 32 pixels: every thread runs
+// the depthwise taps of its (pixel, 8-channel group) items in the order and
+// with the fp32 fma chain of misc.hip's dw8_kernel (taps (dy, dx) ascending,
+// then the bias), splits the result into an LDS image, and the waves run
+// conv2 on it with packed weight fragments streamed from L2 two K chunks
+// ahead (sgemm.hip's products and K order); the epilogue adds b2 and the
+// identity from the accumulators.  Bit-identical to the two unfused launches.
+struct DP {
+  const float *t;
+  int npix, H, W, tcs, tco, tbytes;
+  const float *r;
+  int rcs, rco, rbytes;
+  float *y;
+  int ycs, yco, ybytes;
+  const float *w9, *bdw;   // depthwise taps [9][C], bias [C]
+  const uint16_t *w2;      // conv2 [C][C] as packed fragments
+  int w2bytes;
+  const float *b2;
+};
+
+template <int C>
+__global__ void __launch_bounds__(kNT) sldc_kernel(DP p) {
+  constexpr int KC = C / 32, NTW = C / 64, PF = 2;
+  constexpr int XI = KC * P * 32;
+  extern __shared__ __align__(16) unsigned char smem[];
+  uint16_t *Dh = reinterpret_cast<uint16_t *>(smem), *Dl = Dh + XI;
+  float *Lw9 = reinterpret_cast<float *>(Dl + XI);   // [9][C]
+  float *Lbd = Lw9 + 9 * C, *Lb2 = Lbd + C;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int col = lane & 15, g = lane >> 4;
+  const int pix0 = blockIdx.x * P;
+  const __amdgpu_buffer_rsrc_t tr = rsrc(p.t + p.tco, p.tbytes);
+  const __amdgpu_buffer_rsrc_t w2r = rsrc(p.w2, p.w2bytes);
+
+  f16x8 ah[PF + 1][NTW], al[PF + 1][NTW];
+  auto ldw = [&](int kc, int q) {
+#pragma unroll
+    for (int j = 0; j < NTW; ++j) {
+      const int o = (((wave * NTW + j) * KC + kc) * 1024 + lane * 8) * 2;
+      ah[q][j] = __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(w2r, o, 0, 0));
+      al[q][j] = __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(w2r, o + 1024, 0, 0));
+    }
+  };
+#pragma unroll
+  for (int kc = 0; kc < PF; ++kc) ldw(kc, kc);
+
+  for (int i = tid; i < 9 * C; i += kNT) Lw9[i] = p.w9[i];
+  for (int i = tid; i < C; i += kNT) {
+    Lbd[i] = p.bdw[i];
+    Lb2[i] = p.b2[i];
+  }
+  __syncthreads();
+
+  // depthwise: items (pixel, 8-channel group)
+  for (int u = tid; u < P * C / 8; u += kNT) {
+    const int px = u / (C / 8), c8 = u - px * (C / 8);
+    const int P0 = pix0 + px;
+    const bool okp = P0 < p.npix;
+    const int py = P0 / p.W, pxx = P0 - py * p.W;
+    float acc[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] = 0.f;
+#pragma unroll
+    for (int dy = -1; dy <= 1; ++dy)
+#pragma unroll
+      for (int dx = -1; dx <= 1; ++dx) {
+        const int yy = py + dy, xx = pxx + dx;
+        const bool ok = okp && (unsigned)yy < (unsigned)p.H && (unsigned)xx < (unsigned)p.W;
+        if (!ok) continue;   // (uniform for most items; dw8_kernel skips the out-of-map taps too)
+        const int o = ((yy * p.W + xx) * p.tcs + c8 * 8) * 4;
+        const f32x4 a = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(tr, o, 0, 0));
+        const f32x4 b = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(tr, o + 16, 0, 0));
+        const float *wt = Lw9 + ((dy + 1) * 3 + dx + 1) * C + c8 * 8;
+        const float4 w0 = *reinterpret_cast<const float4 *>(wt), w1 = *reinterpret_cast<const float4 *>(wt + 4);
+        acc[0] = __builtin_fmaf(w0.x, a[0], acc[0]);
+        acc[1] = __builtin_fmaf(w0.y, a[1], acc[1]);
+        acc[2] = __builtin_fmaf(w0.z, a[2], acc[2]);
+        acc[3] = __builtin_fmaf(w0.w, a[3], acc[3]);
+        acc[4] = __builtin_fmaf(w1.x, b[0], acc[4]);
+        acc[5] = __builtin_fmaf(w1.y, b[1], acc[5]);
+        acc[6] = __builtin_fmaf(w1.z, b[2], acc[6]);
+        acc[7] = __builtin_fmaf(w1.w, b[3], acc[7]);
+      }
+    float v[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = okp ? acc[e] + Lbd[c8 * 8 + e] : 0.f;
+    u32x4_t h, l;
+    split8(v, h, l);
+    const int off = swz((c8 >> 2) * P + px, c8 & 3);
+    *reinterpret_cast<u32x4_t *>(Dh + off) = h;
+    *reinterpret_cast<u32x4_t *>(Dl + off) = l;
+  }
+  __syncthreads();
+
+  f32x4 am[NTW][2], ac[NTW][2];
+#pragma unroll
+  for (int j = 0; j < NTW; ++j)
+#pragma unroll
+    for (int pb = 0; pb < 2; ++pb) {
+      am[j][pb] = f32x4{0.f, 0.f, 0.f, 0.f};
+      ac[j][pb] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+  for (int kc = 0; kc < KC; ++kc) {
+    if (kc + PF < KC) ldw(kc + PF, (kc + PF) % (PF + 1));
+    const int q = kc % (PF + 1);
+#pragma unroll
+    for (int pb = 0; pb < 2; ++pb) {
+      const int o = swz(kc * P + pb * 16 + col, g);
+      const f16x8 bh = *reinterpret_cast<const f16x8 *>(Dh + o);
+      const f16x8 bl = *reinterpret_cast<const f16x8 *>(Dl + o);
+#pragma unroll
+      for (int j = 0; j < NTW; ++j) {
+        am[j][pb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[q][j], bh, am[j][pb], 0, 0, 0);
+        ac[j][pb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[q][j], bl, ac[j][pb], 0, 0, 0);
+        ac[j][pb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[q][j], bh, ac[j][pb], 0, 0, 0);
+      }
+    }
+  }
+
+  // epilogue: out = (acc + b2) + identity
+  const __amdgpu_buffer_rsrc_t rr = rsrc(p.r + p.rco, p.rbytes);
+  const __amdgpu_buffer_rsrc_t yr = rsrc(p.y + p.yco, p.ybytes);
+#pragma unroll
+  for (int pb = 0; pb < 2; ++pb) {
+    const int px = pix0 + pb * 16 + col;
+    const bool ok = px < p.npix;
+    f32x4 rv[NTW];
+#pragma unroll
+    for (int j = 0; j < NTW; ++j) {
+      const int n = (wave * NTW + j) * 16 + 4 * g;
+      rv[j] = __builtin_bit_cast(f32x4,
+                                 __builtin_amdgcn_raw_buffer_load_b128(rr, ok ? (px * p.rcs + n) * 4 : kOob, 0, 0));
+    }
+#pragma unroll
+    for (int j = 0; j < NTW; ++j) {
+      const int n = (wave * NTW + j) * 16 + 4 * g;
+      f32x4 v;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = rv[j][e] + ((am[j][pb][e] + ac[j][pb][e] * kLoInv) + Lb2[n + e]);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, v), yr, ok ? (px * p.ycs + n) * 4 : kOob, 0,
+                                             0);
+    }
+  }
+}
+
+template <int C>
+int run_dc(DP p, hipStream_t st) {
+  const size_t lds = (size_t)2 * (C / 32) * P * 32 * 2 + (size_t)11 * C * 4;
+  if (lds > 160 * 1024) return DCVC_HIP_EUNSUPPORTED;
+  const int G = (p.npix + P - 1) / P;
+  auto kern = sldc_kernel<C>;
+  dcvc_note_kernel("sldc_kernel<%d>@%lld", C, (long long)G * kNT);
+  dcvc_ensure_lds(reinterpret_cast<const void *>(kern), 160 * 1024);
+  hipLaunchKernelGGL(kern, dim3((unsigned)G), dim3(kNT), lds, st, p);
+  DCVC_LAUNCH_CHECK();
+  return DCVC_HIP_OK;
+}
+
 template <int C>
 int run(LP p, hipStream_t st) {
   constexpr int KC = C / 32;
@@ -313,4 +482,51 @@ extern "C" int dcvc_internal_lffn(const dcvc_ffn_args *a, void *stream) {
   p.slope = a->slope;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   return a->c == 384 ? run<384>(p, st) : run<192>(p, st);
+}
+
+// MFMA A-fragment packing of an R x K fp32 matrix (R % 16 == 0, K % 32 ==
+// 0): R / 16 x K / 32 fragments of 1024 halves (pack_frags); out NULL: size.
+extern "C" int64_t dcvc_frag_pack_weights(const float *w, int rows, int k, void *out) {
+  if (!w || rows <= 0 || k <= 0 || rows % 16 || k % 32) return DCVC_HIP_EINVAL;
+  const int64_t n = (int64_t)rows * k * 2;
+  if (out) pack_frags(w, rows, k, reinterpret_cast<uint16_t *>(out));
+  return n;
+}
+
+extern "C" int dcvc_dw_conv2_split(const dcvc_dwc_args *a, void *stream) {
+  if (!a || !a->t.ptr || !a->r.ptr || !a->y.ptr || !a->w9 || !a->bdw || !a->w2 || !a->b2) return DCVC_HIP_EINVAL;
+  const int c = a->c;
+  if (a->t.dtype != DCVC_F32 || a->r.dtype != DCVC_F32 || a->y.dtype != DCVC_F32 || a->t.C != c || a->r.C != c ||
+      a->y.C != c || a->t.H != a->y.H || a->t.W != a->y.W || a->r.H != a->y.H || a->r.W != a->y.W)
+    return DCVC_HIP_EINVAL;
+  if (c != 192 && c != 384) return DCVC_HIP_EUNSUPPORTED;
+  auto al = [](const dcvc_tensor &v) { return (uintptr_t)v.ptr % 16 == 0 && v.cstride % 4 == 0 && v.coff % 4 == 0; };
+  if (!al(a->t) || !al(a->r) || !al(a->y) || a->t.cstride % 8 || a->t.coff % 8) return DCVC_HIP_EUNSUPPORTED;
+  const int64_t npix = (int64_t)a->t.H * a->t.W;
+  if (npix <= 0) return DCVC_HIP_OK;
+  auto bytes = [&](const dcvc_tensor &v) { return (npix * v.cstride - v.coff) * 4; };
+  if (bytes(a->t) > 0x7fff0000 || bytes(a->r) > 0x7fff0000 || bytes(a->y) > 0x7fff0000) return DCVC_HIP_EUNSUPPORTED;
+  DP p{};
+  p.t = reinterpret_cast<const float *>(a->t.ptr);
+  p.npix = (int)npix;
+  p.H = a->t.H;
+  p.W = a->t.W;
+  p.tcs = a->t.cstride;
+  p.tco = a->t.coff;
+  p.tbytes = (int)bytes(a->t);
+  p.r = reinterpret_cast<const float *>(a->r.ptr);
+  p.rcs = a->r.cstride;
+  p.rco = a->r.coff;
+  p.rbytes = (int)bytes(a->r);
+  p.y = reinterpret_cast<float *>(a->y.ptr);
+  p.ycs = a->y.cstride;
+  p.yco = a->y.coff;
+  p.ybytes = (int)bytes(a->y);
+  p.w9 = a->w9;
+  p.bdw = a->bdw;
+  p.w2 = reinterpret_cast<const uint16_t *>(a->w2);
+  p.w2bytes = (int)((int64_t)c * c * 2 * 2);
+  p.b2 = a->b2;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  return c == 384 ? run_dc<384>(p, st) : run_dc<192>(p, st);
 }

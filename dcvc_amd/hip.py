@@ -63,6 +63,11 @@ class CDcArgs(ctypes.Structure):
                 ("bdw", ctypes.c_void_p), ("b2", ctypes.c_void_p), ("ba", ctypes.c_void_p), ("slope", ctypes.c_float)]
 
 
+class CDwcArgs(ctypes.Structure):
+    _fields_ = [("t", CTensor), ("r", CTensor), ("y", CTensor), ("c", ctypes.c_int), ("w9", ctypes.c_void_p),
+                ("bdw", ctypes.c_void_p), ("w2", ctypes.c_void_p), ("b2", ctypes.c_void_p)]
+
+
 _T = CTensor
 _vp, _i, _f = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
 HIP_SYMBOLS = [
@@ -75,6 +80,8 @@ HIP_SYMBOLS = [
     ("dcvc_conv_ffn", _i, [ctypes.POINTER(CFfnArgs), _vp]),
     ("dcvc_dc_pack_weights", ctypes.c_int64, [_vp, _vp, _vp, _i, _i, _vp]),
     ("dcvc_depth_conv_split", _i, [ctypes.POINTER(CDcArgs), _vp]),
+    ("dcvc_frag_pack_weights", ctypes.c_int64, [_vp, _i, _i, _vp]),
+    ("dcvc_dw_conv2_split", _i, [ctypes.POINTER(CDwcArgs), _vp]),
     ("dcvc_dwconv3x3", _i, [_T, _T, _vp, _vp, _vp]),
     ("dcvc_flow_warp", _i, [_T, _T, _T, _vp, _vp, _vp]),
     ("dcvc_offset_diversity", _i, [_T, _T, _T, _T, _vp, _vp, _vp, _vp, _f, _vp]),
@@ -442,6 +449,46 @@ class DcW:
         g = lambda t: t.detach().float().contiguous().to(dev)  # noqa: E731
         self.b1, self.w9c, self.bdw, self.b2 = g(b1), g(w9c), g(bdw), g(b2)
         self.ba = g(ba) if wa is not None else None
+
+
+class DwcW:
+    """The tail of a latent DepthConv packed for dcvc_dw_conv2_split: the
+    depthwise taps w9c [9][c] (device) and bias, conv2 [c][c] as MFMA
+    fragments (dcvc_frag_pack_weights) and its bias."""
+
+    def __init__(self, w9c, bdw, w2, b2, device=None):
+        w = w2.detach().float().cpu().reshape(w2.shape[0], -1).contiguous().numpy()
+        self.c = int(w.shape[0])
+        vp = ctypes.c_void_p
+        n = int(check(int(lib().dcvc_frag_pack_weights(w.ctypes.data_as(vp), self.c, self.c, None)), "frag_pack"))
+        host = np.zeros(n, dtype=np.uint16)
+        check(int(lib().dcvc_frag_pack_weights(w.ctypes.data_as(vp), self.c, self.c, host.ctypes.data_as(vp))),
+              "frag_pack")
+        dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
+        self.w2 = torch.from_numpy(host.view(np.int16)).to(dev)
+        g = lambda t: t.detach().float().contiguous().to(dev)  # noqa: E731
+        self.w9c, self.bdw, self.b2 = g(w9c), g(bdw), g(b2)
+
+
+def dw_conv2_split(dwc, t, r, y=None):
+    """y = conv2(dw3x3(t) + bdw) + b2 + r in one kernel (dcvc_dw_conv2_split);
+    None when no kernel is instantiated for the width."""
+    if y is None:
+        y = empty(t.H, t.W, dwc.c, F32, t.buf.device)
+    a = CDwcArgs()
+    a.t, a.r, a.y, a.c = t.c(), r.c(), y.c(), dwc.c
+    a.w9, a.bdw, a.w2, a.b2 = dwc.w9c.data_ptr(), dwc.bdw.data_ptr(), dwc.w2.data_ptr(), dwc.b2.data_ptr()
+    e0 = _t0()
+    rc = lib().dcvc_dw_conv2_split(ctypes.byref(a), stream())
+    if rc == UNSUPPORTED:
+        return None
+    check(rc, "dw_conv2_split")
+    if e0 is not None:
+        n = t.H * t.W
+        kname = lib().dcvc_last_kernel().decode()
+        _t1(e0, kname.split("<")[0], 2 * n * dwc.c * (9 + dwc.c), n * dwc.c * 4 * 3 + dwc.w2.numel() * 2,
+            f"{kname} | dw+conv2 {dwc.c} {t.H}x{t.W} f16x3")
+    return y
 
 
 def depth_conv_split(dw, x, y=None, slope=0.01):

@@ -163,6 +163,12 @@ class DepthConvBlock:
                              sd[d + ".conv2.weight"], sd[d + ".conv2.bias"],
                              sd[d + ".adaptor.weight"] if self.adaptor is not None else None,
                              sd[d + ".adaptor.bias"] if self.adaptor is not None else None, ctx.dev)
+        # split precision, the entropy model's adaptor-free 192 / 384-channel
+        # latent blocks: depthwise + conv2 + identity in one kernel (slffn.hip)
+        self.dwc = None
+        if (FUSE_DC and latent and self.conv1.compute == F16X3 and self.adaptor is None
+                and self.conv1.cin == self.conv2.cout and self.conv2.cin in (192, 384)):
+            self.dwc = K.DwcW(self.dw[0], self.dw[1], sd[d + ".conv2.weight"], sd[d + ".conv2.bias"], ctx.dev)
         self.ffn = None
         # (sffn.hip for the feature-rate widths; slffn.hip for the latent
         # 192 / 384-channel blocks of the entropy model)
@@ -192,8 +198,11 @@ class DepthConvBlock:
             idn = cast(x, dt)
         if dc is None:
             t = K.conv(self.conv1, x, out_dtype=dt, act=ACT_LRELU, slope=self.slope_dc)
-            t = K.dwconv3x3(t, *self.dw)
-            dc = K.conv(self.conv2, t, res=idn)
+            if self.dwc is not None:
+                dc = K.dw_conv2_split(self.dwc, t, idn)
+            if dc is None:
+                t = K.dwconv3x3(t, *self.dw)
+                dc = K.conv(self.conv2, t, res=idn)
         if self.gated:
             h = K.conv(self.ffn1, dc)
             return K.conv(self.ffn2, h, y, in_op=IN_GATE, in_slope=self.slope_ffn, res=dc, scale=scale)

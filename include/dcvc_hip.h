@@ -161,6 +161,28 @@ int64_t dcvc_ffn_pack_weights(const float *w1, const float *w2, int c, int hidde
 int dcvc_conv_ffn(const dcvc_ffn_args *a, void *stream);
 
 /*
+ * The tail of a latent DepthConv in split-fp16 arithmetic,
+ * DCVC-DC/src/models/layers.py:135-163 for the adaptor-free C -> C blocks
+ * of the entropy model (video_model.py:250-305, c in {192, 384}):
+ *   y = conv2(dw3x3(t) + bdw) + b2 + r
+ * t = lrelu(conv1(x) + b1) (the previous dcvc_conv2d), r = the block input.
+ * w9 = depthwise taps [9][c] fp32 (tap (dy, dx) at (dy + 1) * 3 + dx + 1),
+ * w2 = conv2 [c][c] packed by dcvc_frag_pack_weights (16 x 32 MFMA
+ * fragments, hi and lo planes; out NULL returns the element count).
+ * Replaces the depthwise launch and the conv2 launch of the unfused block
+ * with identical results.  DCVC_HIP_EUNSUPPORTED for other widths.
+ */
+typedef struct dcvc_dwc_args {
+  dcvc_tensor t, r, y;
+  int c;
+  const float *w9, *bdw;
+  const void *w2;
+  const float *b2;
+} dcvc_dwc_args;
+int64_t dcvc_frag_pack_weights(const float *w, int rows, int k, void *out);
+int dcvc_dw_conv2_split(const dcvc_dwc_args *a, void *stream);
+
+/*
  * Fused DepthConv in split-fp16 arithmetic (Precision.split()),
  * DCVC-DC/src/models/layers.py:135-163:
  *   y = conv2(dw3x3(lrelu(conv1(x) + b1, slope) + ...) + bdw) + b2 + identity,

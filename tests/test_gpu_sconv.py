@@ -350,6 +350,39 @@ def test_latent_ffn_matches_fp64_and_unfused(c, H, W):
     assert torch.equal(y2.nchw().cpu(), got)
 
 
+@pytest.mark.parametrize("c,H,W", [(384, 68, 120), (192, 68, 120), (384, 17, 30), (192, 5, 7), (384, 1, 40)])
+def test_latent_dw_conv2_matches_fp64_and_unfused(c, H, W):
+    """sldc_kernel (slffn.hip): the tail of a latent DepthConv, conv2(dw3x3(t)
+    + bdw) + b2 + x (DCVC-DC/src/models/layers.py:135-163), against fp64 and
+    bit-identical to the unfused depthwise + split-fp16 GEMM launches; image
+    edges, ragged 32-pixel tiles spanning rows, channel views."""
+    h = K()
+    g = torch.Generator().manual_seed(c * 3 + H * W)
+    tb = torch.randn(1, c + 8, H, W, generator=g)
+    xb = torch.randn(1, c + 16, H, W, generator=g)
+    wd = torch.randn(c, 1, 3, 3, generator=g) / 3
+    bd = torch.randn(c, generator=g) * 0.1
+    w2 = torch.randn(c, c, 1, 1, generator=g) / c ** 0.5
+    b2 = torch.randn(c, generator=g) * 0.1
+    t, x = tb[:, 8:], xb[:, 4:4 + c]
+    ref = F.conv2d(F.conv2d(t.double(), wd.double(), bd.double(), padding=1, groups=c), w2.double(), b2.double()) \
+        + x.double()
+    w9c = wd.reshape(c, 9).t().contiguous()
+    dwc = h.DwcW(w9c, bd, w2, b2)
+    ta = h.from_nchw(tb, h.F32).ch(8, c)
+    xa = h.from_nchw(xb, h.F32).ch(4, c)
+    out = h.empty(H, W, c + 4, h.F32)
+    y = h.dw_conv2_split(dwc, ta, xa, out.ch(4, c))
+    torch.cuda.synchronize()
+    assert y is not None and h.lib().dcvc_last_kernel().decode().startswith("sldc_kernel")
+    got = out.ch(4, c).nchw().cpu()
+    assert rel_err(got, ref) < TOL
+    d = h.dwconv3x3(ta, w9c.cuda(), bd.cuda())
+    y2 = h.conv(h.ConvW(w2, b2, 1, h.F16X3), d, res=xa)
+    torch.cuda.synchronize()
+    assert torch.equal(y2.nchw().cpu(), got)
+
+
 @pytest.mark.parametrize("cin,cout,adapt,H,W", [(64, 48, True, 37, 53), (48, 32, True, 20, 33), (32, 64, True, 17, 16),
                                                 (64, 64, False, 9, 70), (48, 48, False, 8, 16), (32, 32, False, 25, 31)])
 def test_fused_depthconv_matches_fp64(cin, cout, adapt, H, W):
