@@ -492,6 +492,29 @@ def pmc_traffic(kname, workload):
     return None
 
 
+def pmc_layer_traffic(kname, layer, nbytes):
+    """HBM bytes per launch of one layer shape from a committed per-layer PMC
+    record (profiles/*_pmc_layers.json, scripts/pmc_layer.sh: the split conv
+    microbenchmark of that shape under separate FETCH_SIZE / WRITE_SIZE
+    passes), for a dominant kernel whose whole-frame PMC average mixes layer
+    shapes; matched by instantiation@grid, layer key and algorithmic bytes
+    (within 1 %, which tells a residual from none)."""
+    import glob
+    for path in sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)),
+                                              "profiles", "*_pmc_layers.json")), reverse=True):
+        try:
+            with open(path) as f:
+                d = json.load(f)
+        except (OSError, ValueError):
+            continue
+        for e in d.get("layers", []):
+            if (e.get("kernel") == kname and e.get("layer") == layer
+                    and abs(e.get("algorithmic_bytes_no_weights", 0) - nbytes) <= 0.01 * nbytes):
+                return {"hbm_bytes_per_launch": e["hbm_bytes_per_launch"], "source": os.path.basename(path),
+                        "rocprof_avg_launch_us": e.get("avg_us")}
+    return None
+
+
 def heartbeat(period=60.0):
     """A line on stderr every `period` seconds while the bench runs (long CPU
     baseline samples would otherwise look like a hung process to a watchdog
@@ -719,6 +742,12 @@ def main():
                 roof["traffic"] = None
                 roof["traffic_note"] = ("PMC summary of this instantiation@grid averages several layer shapes "
                                         f"(rocprof {tr['rocprof_avg_launch_us']} us vs {ev:.1f} us for this layer)")
+                lt = pmc_layer_traffic(kname, shape, nb / n)
+                if lt:
+                    roof["traffic"] = lt["hbm_bytes_per_launch"]
+                    roof["traffic_source"] = lt["source"]
+                    roof["traffic_note"] += (f"; traffic from the per-layer PMC record of this shape "
+                                             f"(microbenchmark {lt['rocprof_avg_launch_us']} us per launch)")
         roof["kernel"] = kname
         roof["layer"] = shape
         roof["launches_per_P_frame"] = n
