@@ -507,11 +507,22 @@ def pmc_layer_traffic(kname, layer, nbytes):
                 d = json.load(f)
         except (OSError, ValueError):
             continue
-        for e in d.get("layers", []):
-            if (e.get("kernel") == kname and e.get("layer") == layer
-                    and abs(e.get("algorithmic_bytes_no_weights", 0) - nbytes) <= 0.01 * nbytes):
+        recs = [e for e in d.get("layers", []) if e.get("kernel") == kname and e.get("layer") == layer]
+        for e in recs:
+            if abs(e.get("algorithmic_bytes_no_weights", 0) - nbytes) <= 0.01 * nbytes:
                 return {"hbm_bytes_per_launch": e["hbm_bytes_per_launch"], "source": os.path.basename(path),
                         "rocprof_avg_launch_us": e.get("avg_us")}
+        # the layer key's launches mix calls with and without a residual: the
+        # traffic of that mix is linear in the mix, as the algorithmic bytes are
+        plain = [e for e in recs if not e.get("residual")]
+        resid = [e for e in recs if e.get("residual")]
+        if plain and resid:
+            b0, b1 = plain[0]["algorithmic_bytes_no_weights"], resid[0]["algorithmic_bytes_no_weights"]
+            if b0 < nbytes < b1:
+                f = (nbytes - b0) / (b1 - b0)
+                t = plain[0]["hbm_bytes_per_launch"] * (1 - f) + resid[0]["hbm_bytes_per_launch"] * f
+                return {"hbm_bytes_per_launch": int(t), "source": os.path.basename(path),
+                        "rocprof_avg_launch_us": None, "mix_residual_fraction": round(f, 3)}
     return None
 
 
@@ -746,8 +757,9 @@ def main():
                 if lt:
                     roof["traffic"] = lt["hbm_bytes_per_launch"]
                     roof["traffic_source"] = lt["source"]
-                    roof["traffic_note"] += (f"; traffic from the per-layer PMC record of this shape "
-                                             f"(microbenchmark {lt['rocprof_avg_launch_us']} us per launch)")
+                    roof["traffic_note"] += ("; traffic from the per-layer PMC records of this shape (microbenchmark"
+                                             + (f", {lt['mix_residual_fraction']} of the launches with a residual"
+                                                if "mix_residual_fraction" in lt else "") + ")")
         roof["kernel"] = kname
         roof["layer"] = shape
         roof["launches_per_P_frame"] = n
