@@ -280,7 +280,7 @@ int launch(GP p, hipStream_t st) {
 // 1..6 = force (BN, PXW) = (128, 2), (64, 2), (32, 2), (128, 1), (64, 1), (32, 1)
 int g_cfg = 0;
 int g_cus = 0;
-int g_pd = 0;   // dcvc_set_option("sgemm_pd", 2 | 3 | 5): stages in flight (A/B); 0 = auto
+int g_pd = 0;   // dcvc_set_option("sgemm_pd", 1 | 2 | 3 | 5): stages in flight (A/B); 0 = auto
 
 template <int PD>
 int run_pd(int cfg, const GP &p, hipStream_t st) {
@@ -294,12 +294,14 @@ int run_pd(int cfg, const GP &p, hipStream_t st) {
     default: return DCVC_HIP_EUNSUPPORTED;
   }
 }
-// auto: 3 stages in flight, 2 when the K walk has at most 2 chunks (the
-// third buffer would only hold zeros, and the smaller LDS footprint lets two
-// workgroups share a CU: the short tiles of e.g. 48 -> 48 at 1080p are
-// latency-bound, one stage of DMA and an epilogue each)
+// auto: 2 stages in flight.  Three buffers instead of four let two
+// workgroups share a CU, and a second workgroup hides a tile's DMA latency
+// and epilogue better than a deeper ring: measured on the codec's 1x1 layers
+// (scripts/gpu_r03za.sh), 384 -> 384 at 68x120 25.5 -> 17.7 us, 96 -> 48 at
+// 1080p 394 -> 272 us, 128 -> 64 at 544x960 148 -> 120 us
 int run_cfg(int cfg, const GP &p, hipStream_t st) {
-  const int pd = g_pd ? g_pd : (p.nchunks <= 2 ? 2 : 3);
+  const int pd = g_pd ? g_pd : 2;
+  if (pd == 1) return run_pd<1>(cfg, p, st);
   if (pd == 2) return run_pd<2>(cfg, p, st);
   if (pd == 5) return run_pd<5>(cfg, p, st);
   return run_pd<3>(cfg, p, st);

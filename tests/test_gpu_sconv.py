@@ -107,12 +107,37 @@ def test_sgemm_matches_fp64(cfg, cin, cout, H, W):
         y = h.conv(cw, h.from_nchw(x, h.F32), out_dtype=h.F32)
         torch.cuda.synchronize()
         bn, pxw = SGEMM_CFGS[cfg]
-        # 3 stages in flight, 2 for K walks of at most 2 chunks (cin <= 64)
-        assert h.lib().dcvc_last_kernel().decode() == f"sgemm_kernel<{bn}, {pxw}, {2 if cin <= 64 else 3}>"
+        assert h.lib().dcvc_last_kernel().decode() == f"sgemm_kernel<{bn}, {pxw}, 2>"
     finally:
         h.set_option("sgemm", 0)
     err = rel_err(y.nchw().cpu(), ref)
     assert err < TOL, err
+
+
+@pytest.mark.parametrize("pd", [1, 2, 3, 5])
+def test_sgemm_stage_depths(pd):
+    """sgemm.hip with 1, 2, 3 and 5 stages in flight: same products and K order,
+    so bit-identical to each other, and within the fp64 bound."""
+    h = K()
+    g = torch.Generator().manual_seed(pd)
+    cin, cout, H, W = 384, 192, 17, 30
+    x = torch.randn(1, cin, H, W, generator=g)
+    w = torch.randn(cout, cin, 1, 1, generator=g) / cin ** 0.5
+    b = torch.randn(cout, generator=g) * 0.1
+    ref = F.conv2d(x.double(), w.double(), b.double())
+    cw = h.ConvW(w, b, 1, h.F16X3)
+    xa = h.from_nchw(x, h.F32)
+    h.set_option("sgemm_pd", pd)
+    try:
+        y = h.conv(cw, xa, out_dtype=h.F32)
+        torch.cuda.synchronize()
+        assert h.lib().dcvc_last_kernel().decode().endswith(f", {pd}>")
+    finally:
+        h.set_option("sgemm_pd", 0)
+    y0 = h.conv(cw, xa, out_dtype=h.F32)
+    torch.cuda.synchronize()
+    assert rel_err(y.nchw().cpu(), ref) < TOL
+    assert torch.equal(y.nchw().cpu(), y0.nchw().cpu())
 
 
 @pytest.mark.parametrize("cfg", [0, 2, 6])
