@@ -583,14 +583,17 @@ int g_resident = 1;   // dcvc_set_option("sconv_resident", 0): streamed weights 
 
 // tile rows per wave: the tallest tile that still gives >= 1.5 tiles per CU
 // and whose image prefetch fits the registers, else the smallest
+int g_rw = 0;   // dcvc_set_option("sconv_rw", 1 | 2 | 4): force the tile rows per wave (A/B; 0 = auto)
+
 template <int KS, int S, int BN, int NW, bool GATE, bool RES>
 int pick_rw_nw(SP p, hipStream_t st) {
   const int64_t tx = (p.Wo + 15) / 16, nb = (p.cout + BN - 1) / BN;
-  auto tiles = [&](int th) { return tx * ((p.Ho + th - 1) / th) * nb; };
+  auto tiles = [&](int th) { return g_rw ? 384 : tx * ((p.Ho + th - 1) / th) * nb; };
   constexpr int PMAX = NW == 8 ? 5 : 8;   // image pieces per thread the registers allow
+  if (g_rw == 1) return launch<KS, S, BN, 1, NW, GATE, RES>(p, st);
   if constexpr (SG<KS, S, BN, 4, NW, RES>::LDS <= 160 * 1024 && SG<KS, S, BN, 4, NW, RES>::PPI <= PMAX &&
                 !(NW == 4 && KS == 3 && BN == 64)) {
-    if (tiles(4 * NW) >= 384) {
+    if (tiles(4 * NW) >= 384 && g_rw != 2) {
       const int r = launch<KS, S, BN, 4, NW, GATE, RES>(p, st);
       if (r != DCVC_HIP_EUNSUPPORTED) return r;
     }
@@ -664,6 +667,7 @@ int pick_bn(SP p, hipStream_t st) {
 
 extern "C" void dcvc_internal_sconv_occupancy(int v) { g_occ = v; }
 extern "C" void dcvc_internal_sconv_dbg(int v) { g_dbg = v; }
+extern "C" void dcvc_internal_sconv_rw(int v) { g_rw = v; }
 extern "C" int dcvc_internal_sgemm(const dcvc_conv_args *a, void *stream);
 extern "C" int dcvc_internal_sconvr(const dcvc_conv_args *a, void *stream);
 extern "C" void dcvc_internal_sconv_waves(int v) { g_waves = v; }

@@ -417,6 +417,7 @@ int launch_nt(RP p, int nt, int nres, hipStream_t st) {
 }  // namespace
 
 extern "C" void dcvc_internal_sconv_dbg(int v);
+extern "C" void dcvc_internal_sconv_rw(int v);
 
 // options of the split-precision kernels (dcvc_set_option falls through to
 // here, so adding one does not rebuild conv.hip)
@@ -425,6 +426,7 @@ extern "C" int dcvc_internal_set_option_split(const char *name, int value) {
   else if (std::strcmp(name, "sconvr_nt") == 0) g_force_nt = value;
   else if (std::strcmp(name, "sconvr_waves") == 0) g_waves = value;
   else if (std::strcmp(name, "sconv_dbg") == 0) dcvc_internal_sconv_dbg(value);
+  else if (std::strcmp(name, "sconv_rw") == 0) dcvc_internal_sconv_rw(value);
   else return DCVC_HIP_EINVAL;
   return DCVC_HIP_OK;
 }
