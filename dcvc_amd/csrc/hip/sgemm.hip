@@ -52,6 +52,7 @@ struct GP {
   int rcs, rco;
   const float *res2;
   int r2cs, r2co;
+  int shuffle, W;   // pixel shuffle (x2) on store: the input map's width W
 };
 
 template <int BN, int PXW, int PD>
@@ -94,7 +95,7 @@ __global__ void __launch_bounds__(256) sgemm_kernel(GP p) {
   for (int i = tid; i < BN; i += 256) {
     const int n = n0 + i;
     Lc[i] = (p.bias && n < p.cout) ? p.bias[n] : 0.f;
-    Lc[BN + i] = (p.scale && n < p.cout) ? p.scale[n] : 1.f;
+    Lc[BN + i] = (p.scale && n < p.cout) ? p.scale[p.shuffle ? n / 4 : n] : 1.f;
   }
 
   // Both operands arrive by LDS-DMA (16 bytes per lane, lane-linear LDS
@@ -207,6 +208,36 @@ __global__ void __launch_bounds__(256) sgemm_kernel(GP p) {
   }
   wait_vm_lgkm();   // the zero-fill pieces past the last stage: no LDS-DMA in flight at exit
 
+  if (p.shuffle) {
+    // pixel shuffle (subpel_conv1x1, r = 2): conv channels n .. n + 3 (n % 4
+    // == 0) of pixel (oy, ox) go to output channel n / 4 of the 2x2 block
+    // (2 oy + (e >> 1), 2 ox + (e & 1)); residuals and the scale are indexed in
+    // the output map, bias and activation per conv channel (epilogue.h order)
+#pragma unroll
+    for (int r = 0; r < PXW; ++r) {
+      const int P = pix0 + (wave * PXW + r) * 16 + col;
+      const bool okp = P < p.npix;
+      const int oy = P / p.W, ox = P - (P / p.W) * p.W;
+#pragma unroll
+      for (int jn = 0; jn < NT; ++jn) {
+        const int nl = jn * 16 + hi * 4, n = n0 + nl;
+        if (!okp || n >= p.cout) continue;
+        const float4 bb = *reinterpret_cast<const float4 *>(Lc + nl);
+        const float bv[4] = {bb.x, bb.y, bb.z, bb.w};
+        const float sc = Lc[BN + nl];   // scale[n / 4] staged at the n-block's channel nl (below)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int64_t q = (int64_t)(2 * oy + (e >> 1)) * (2 * p.W) + 2 * ox + (e & 1);
+          float v = apply_act(p.act, (am[r][jn][e] + ac[r][jn][e] * kLoInv) + bv[e], p.slope);
+          if (p.res) v = p.res[q * p.rcs + p.rco + n / 4] + v;
+          if (p.res2) v = p.res2[q * p.r2cs + p.r2co + n / 4] + v;
+          if (p.scale) v *= sc;
+          p.y[q * p.ycs + p.yco + n / 4] = v;
+        }
+      }
+    }
+    return;
+  }
   // epilogue: lane (col, hi) of fragment (r, jn) holds output channels
   // n0 + 16 jn + 4 hi .. + 3 of pixel (wave * PXW + r) * 16 + col
 #pragma unroll
@@ -317,10 +348,12 @@ extern "C" void dcvc_internal_sgemm_pd(int v) { g_pd = v; }
 // DCVC_HIP_EUNSUPPORTED sends the call back to sconv.hip.
 extern "C" int dcvc_internal_sgemm(const dcvc_conv_args *a, void *stream) {
   if (g_cfg < 0) return DCVC_HIP_EUNSUPPORTED;
-  if (a->kh != 1 || a->kw != 1 || a->stride != 1 || a->pad != 0 || a->shuffle) return DCVC_HIP_EUNSUPPORTED;
+  if (a->kh != 1 || a->kw != 1 || a->stride != 1 || a->pad != 0) return DCVC_HIP_EUNSUPPORTED;
   if (a->in_op != DCVC_IN_NONE && a->in_op != DCVC_IN_LRELU) return DCVC_HIP_EUNSUPPORTED;
   if (a->x.dtype != DCVC_F32 || a->y.dtype != DCVC_F32) return DCVC_HIP_EUNSUPPORTED;
-  if (a->x.H != a->y.H || a->x.W != a->y.W) return DCVC_HIP_EUNSUPPORTED;
+  const int f = a->shuffle ? 2 : 1;
+  if (a->x.H * f != a->y.H || a->x.W * f != a->y.W) return DCVC_HIP_EUNSUPPORTED;
+  if (a->shuffle && (a->cout % 4 || a->y.C * 4 != a->cout)) return DCVC_HIP_EUNSUPPORTED;
   auto al = [](const void *ptr, int cs, int co) {
     return ptr == nullptr || ((uintptr_t)ptr % 16 == 0 && cs % 4 == 0 && co % 4 == 0);
   };
@@ -347,6 +380,8 @@ extern "C" int dcvc_internal_sgemm(const dcvc_conv_args *a, void *stream) {
     if (wb >= ((int64_t)1 << 31) - 64) return DCVC_HIP_EUNSUPPORTED;
     p.wbytes = (int)wb;
   }
+  p.shuffle = a->shuffle ? 1 : 0;
+  p.W = a->x.W;
   p.bias = a->bias;
   p.y = reinterpret_cast<float *>(a->y.ptr);
   p.ycs = a->y.cstride;

@@ -114,6 +114,44 @@ def test_sgemm_matches_fp64(cfg, cin, cout, H, W):
     assert err < TOL, err
 
 
+@pytest.mark.parametrize("cfg", [0, 1, 5])
+@pytest.mark.parametrize("cin,cout,H,W", [(64, 256, 13, 21), (128, 256, 9, 40), (64, 128, 17, 16)])
+def test_sgemm_pixel_shuffle(cfg, cin, cout, H, W):
+    """sgemm.hip's pixel-shuffle epilogue (subpel_conv1x1, DCVC-DC/src/models/
+    layers.py:26-31 as the hyperprior decoders and upsamplers use it): bias and
+    activation per conv channel, then residuals and the scale in the output
+    map, on channel views; against fp64 and the sconv.hip 1x1 path."""
+    h = K()
+    g = torch.Generator().manual_seed(cin + cout + H + cfg)
+    x = torch.randn(1, cin, H, W, generator=g)
+    w = torch.randn(cout, cin, 1, 1, generator=g) / cin ** 0.5
+    b = torch.randn(cout, generator=g) * 0.1
+    co = cout // 4
+    r = torch.randn(1, co, 2 * H, 2 * W, generator=g)
+    sc = torch.rand(co, generator=g) + 0.5
+    ref = (r.double() + F.pixel_shuffle(F.leaky_relu(F.conv2d(x.double(), w.double(), b.double()), 0.1), 2)) \
+        * sc.double().view(1, -1, 1, 1)
+    cw = h.ConvW(w, b, 1, h.F16X3)
+    xa = h.from_nchw(x, h.F32)
+    ra = h.from_nchw(r, h.F32)
+    outs = []
+    for opt in (cfg, -1):
+        out = h.empty(2 * H, 2 * W, co + 8, h.F32)
+        out.buf.fill_(7.0)
+        h.set_option("sgemm", opt)
+        try:
+            h.conv(cw, xa, out.ch(4, co), shuffle=True, act=h.ACT_LRELU, slope=0.1, res=ra, scale=sc.cuda())
+            torch.cuda.synchronize()
+            kern = h.lib().dcvc_last_kernel().decode()
+        finally:
+            h.set_option("sgemm", 0)
+        assert kern.startswith("sgemm_kernel" if opt >= 0 else "sconv_kernel"), kern
+        assert bool((out.buf[:, :, :4] == 7.0).all()) and bool((out.buf[:, :, 4 + co:] == 7.0).all())
+        outs.append(out.ch(4, co).nchw().cpu())
+    assert rel_err(outs[0], ref) < TOL
+    assert rel_err(outs[1], ref) < TOL
+
+
 @pytest.mark.parametrize("pd", [1, 2, 3, 5])
 def test_sgemm_stage_depths(pd):
     """sgemm.hip with 1, 2, 3 and 5 stages in flight: same products and K order,
