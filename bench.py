@@ -204,7 +204,7 @@ def oracle_ip_times(isd, psd, args, threads, capture=None):
     def code(calls, pre):
         cc = [(s.clamp(-30000, 30000).to(torch.int16).numpy(), i.to(torch.int16).numpy(), tabs[pre + k])
               for k, s, i in calls]
-        enc = R.DCStream()
+        enc = R.DCStream(args.stream_part)   # the product's part count, so the stream bytes compare
         st = enc.encode(cc)
         nbytes.append(len(st))
         dec = enc.decode(st)
