@@ -647,10 +647,11 @@ int pick_bn(SP p, hipStream_t st) {
       bn_order(p.cout, 64, order);
       for (int i = 0; i < 4 && order[i]; ++i) {
         // a 16-channel resident n-block of a wide layer re-reads and re-splits
-        // the input once per n-block (6+ times): streamed 64-channel blocks win
-        // there (128 -> 192 at 544x960: 1063 -> 969 us), not at 3-4 n-blocks
-        // (96 -> 48 at 1080p: 868 vs 1164 us; scripts/gpu_r03zd.sh)
-        if (KS == 3 && order[i] == 16 && (p.cout + 15) / 16 >= 6) continue;
+        // the input once per n-block (8+ times): streamed 64-channel blocks win
+        // there (128 -> 192 at 544x960: 1063 -> 969 us, 192 -> 256 at 272x480:
+        // 742 -> 462 us), not at 3-6 n-blocks (96 -> 48 at 1080p: 868 vs 1164
+        // us, 192 -> 96 at 272x480: 258 vs 370 us; scripts/gpu_r03zd.sh, r03zf)
+        if (KS == 3 && order[i] == 16 && (p.cout + 15) / 16 >= 8) continue;
         const int nw = g_res_waves ? g_res_waves : (KS == 1 ? 4 : 8);
         const int r = nw == 4 ? try_bn<KS, S, GATE, true, 4>(p, order[i], st)
                               : try_bn<KS, S, GATE, true, 8>(p, order[i], st);
