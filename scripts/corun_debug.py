@@ -48,7 +48,7 @@ def main():
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     isd, psd = bench.make_weights(None, 0, dev, "dc")
-    prec = Precision.fast() if args.precision == "fast" else Precision.parity()
+    prec = {"fast": Precision.fast, "split": Precision.split, "parity": Precision.parity}[args.precision]()
     h, w = 1080, 1920
     log = {"cur": None}
 

@@ -17,10 +17,14 @@ pytestmark = pytest.mark.gpu
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def test_two_codec_processes_share_the_gpu():
+@pytest.mark.parametrize("precision", ["split", "fast"])
+def test_two_codec_processes_share_the_gpu(precision):
+    """split: the bench precision (its kernels co-run at the default 3 GOP
+    lanes); fast: the bf16 kernels the failure was first seen with."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
-    cmd = [sys.executable, os.path.join(REPO, "scripts", "corun_debug.py"), "--frames", "12"]
+    cmd = [sys.executable, os.path.join(REPO, "scripts", "corun_debug.py"), "--frames", "12",
+           "--precision", precision]
     env = dict(os.environ)
     procs = [subprocess.Popen(cmd, cwd=REPO, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
              for _ in range(2)]
