@@ -583,6 +583,9 @@ extern "C" void dcvc_internal_sconv_res_waves(int v);
 extern "C" void dcvc_internal_sgemm_cfg(int v);
 extern "C" void dcvc_internal_sgemm_pd(int v);
 extern "C" int dcvc_internal_set_option_split(const char *name, int value);
+extern "C" int dcvc_internal_xconv(const dcvc_conv_args *a, void *stream);
+extern "C" void dcvc_internal_xconv_enable(int v);
+extern "C" void dcvc_internal_xconv_waves(int v);
 
 extern "C" int dcvc_conv2d(const dcvc_conv_args *a, void *stream) {
   if (!a || !a->w || !valid_view(a->x) || !valid_view(a->y)) return DCVC_HIP_EINVAL;
@@ -635,7 +638,11 @@ extern "C" int dcvc_conv2d(const dcvc_conv_args *a, void *stream) {
     p.r2cs = a->res2.cstride;
     p.r2co = a->res2.coff;
   }
-  if (a->compute == DCVC_F16X3) return dcvc_internal_sconv(a, stream);   // the split-fp16 kernels only
+  if (a->compute == DCVC_F16X3) {   // the split-fp16 kernels only
+    const int r = dcvc_internal_xconv(a, stream);   // static-shape 3x3 stride-1 kernel (xconv.hip)
+    if (r != DCVC_HIP_EUNSUPPORTED) return r;
+    return dcvc_internal_sconv(a, stream);
+  }
   if (a->compute != DCVC_F32 && a->compute != DCVC_BF16) return DCVC_HIP_EINVAL;
   if (a->kh == 3 && a->kw == 3 && a->stride == 1 && a->compute == DCVC_BF16 && g_use_conv3) {
     const int r = dcvc_internal_conv3x3(a, stream);
@@ -783,9 +790,17 @@ extern "C" int dcvc_set_option(const char *name, int value) {
     dcvc_internal_sconv_occupancy(value);
     return DCVC_HIP_OK;
   }
+  if (std::strcmp(name, "xconv") == 0) {
+    dcvc_internal_xconv_enable(value);
+    return DCVC_HIP_OK;
+  }
+  if (std::strcmp(name, "xconv_waves") == 0) {
+    dcvc_internal_xconv_waves(value);
+    return DCVC_HIP_OK;
+  }
   if (std::strcmp(name, "conv3x3_rows4") == 0) {
     dcvc_internal_conv3p_rows4(value);
     return DCVC_HIP_OK;
   }
-  return dcvc_internal_set_option_split(name, value);   // the split-precision kernels' options (sconvr.hip)
+  return dcvc_internal_set_option_split(name, value);   // the split-precision kernels' options (xconv.hip)
 }

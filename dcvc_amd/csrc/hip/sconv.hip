@@ -564,8 +564,11 @@ int launch(SP p, hipStream_t st) {
   if (g_occ > 0 && g_occ < per_cu) per_cu = g_occ;
   int64_t G = (int64_t)g_cus * per_cu;
   if (G > nt) G = nt;
-  // a workgroup keeps one n-block (resident weights): the grid stride is a
-  // multiple of the n-block count, and of 8 for the XCD remap when it can be
+  // a workgroup keeps one n-block (resident weights, loaded once): the grid
+  // stride must be a multiple of the n-block count.  A grid smaller than the
+  // n-block count (few CUs, or the sconv_occupancy option) cannot keep that:
+  // the caller then takes the streamed-weight kernel
+  if (RES && G < p.nblk) return DCVC_HIP_EUNSUPPORTED;
   if (RES && G % p.nblk) G = G / p.nblk * p.nblk;
   if (G < 1) G = 1;
   auto kern = sconv_kernel<KS, S, BN, RW, NW, GATE, RES>;
@@ -675,7 +678,6 @@ extern "C" void dcvc_internal_sconv_occupancy(int v) { g_occ = v; }
 extern "C" void dcvc_internal_sconv_dbg(int v) { g_dbg = v; }
 extern "C" void dcvc_internal_sconv_rw(int v) { g_rw = v; }
 extern "C" int dcvc_internal_sgemm(const dcvc_conv_args *a, void *stream);
-extern "C" int dcvc_internal_sconvr(const dcvc_conv_args *a, void *stream);
 extern "C" void dcvc_internal_sconv_waves(int v) { g_waves = v; }
 extern "C" void dcvc_internal_sconv_resident(int v) { g_resident = v; }
 extern "C" void dcvc_internal_sconv_res_waves(int v) { g_res_waves = v; }
@@ -690,10 +692,6 @@ extern "C" int dcvc_internal_sconv(const dcvc_conv_args *a, void *stream) {
   if (a->in_op == DCVC_IN_GATE && a->kh != 1) return DCVC_HIP_EUNSUPPORTED;
   if (a->kh == 1) {   // the pixel-GEMM kernel (sgemm.hip) where it applies
     const int r = dcvc_internal_sgemm(a, stream);
-    if (r != DCVC_HIP_EUNSUPPORTED) return r;
-  }
-  if (a->kh == 3 && a->stride == 1) {   // the register-image kernel (sconvr.hip) where it applies
-    const int r = dcvc_internal_sconvr(a, stream);
     if (r != DCVC_HIP_EUNSUPPORTED) return r;
   }
   SP p{};

@@ -1,0 +1,673 @@
+// Static-shape split-fp16 3x3 stride-1 convolution: the feature-rate 3x3
+// layers of Precision.split() (ResBlocks, context fusion, UNet / recon convs
+// of DCVC-DC/src/models/video_net.py:58-76, 129-170 and video_model.py:89-118,
+// 173-232).  Same arithmetic as sconv.hip (x * w ~ xh*wh + 2^-11 (xh*wl +
+// xl*wh) on v_mfma_f32_16x16x32_f16, fp32 accumulation, the same K order and
+// the same epilogue), so the outputs are bit-identical to sconv_kernel's.
+//
+// What differs is the schedule.  sconv.hip carries the channel count, chunk
+// count and tap packing at run time; hipcc then keeps the stage loop as a
+// chain of run-time branches with the accumulators copied at every merge and
+// spills SGPRs into VGPR lanes (~5 VALU per MFMA, MFMA busy ~30 %).  Here CIN,
+// the n-block BN and the tile are template parameters, the K walk of a tile is
+// unrolled at compile time, and every stage has the same shape:
+//
+//   stage = one K step of 32 (one tap of a 32-channel chunk, or 2 / 4 packed
+//           taps of a 16- / 8-channel last chunk), one workgroup barrier;
+//   weights: streamed through a ring of three LDS slots by LDS-DMA, issued
+//           two stages ahead (L2-resident: every tile reads the same weights);
+//   operands: the next stage's A (weights) and B (image) fragments are read
+//           from LDS while the current stage's MFMAs run (two register sets),
+//           so no wave waits on LDS latency at a stage start;
+//   image:  two LDS buffers (hi / lo f16 images, XOR-swizzled); the next
+//           chunk's input pieces are loaded into registers at a chunk's first
+//           stage and split into the other buffer at its second-to-last, so
+//           the publish VALU runs between MFMAs and never behind a barrier;
+//   residual / second residual: loaded into registers at the tile's first
+//           stage, consumed by the epilogue straight from the accumulators.
+//
+// Every vector-memory instruction of a stage is issued unconditionally (buffer
+// loads / stores with out-of-range offsets where there is nothing to move), so
+// the count of vector-memory operations younger than a stage's weight DMA is a
+// compile-time constant and the DMA is waited for with an exact vmcnt(N) that
+// never drains the younger image / residual loads.
+#include "common.h"
+#include "split.h"
+
+#include <algorithm>
+#include <cstring>
+#include <utility>
+
+namespace {
+
+struct XP {
+  const float *x;
+  int H, W, xcs, xco;
+  const uint16_t *w;       // DCVC_F16X3 packed weights (dcvc_conv_pack_weights)
+  float *y;
+  int Ho, Wo, ycs, yco;
+  int cout;
+  int in_lrelu;
+  float in_slope;
+  int act;
+  float slope;
+  const float *res;
+  int rcs, rco;
+  const float *res2;
+  int r2cs, r2co;
+  int has_res, has_res2;
+  int tiles_x, nblk, ntiles;
+  int wbytes;
+  int64_t wchunk;          // halves of one full chunk's packed weights (hi + lo)
+  const float *bias;
+  const float *scale;
+};
+
+template <typename F, int... I>
+__device__ __forceinline__ void sfor_(F &&f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, typename F>
+__device__ __forceinline__ void sfor(F &&f) {
+  sfor_(f, std::make_integer_sequence<int, N>{});
+}
+
+template <int CIN, int BN, int RW, int NW, bool R2>
+struct XG {
+  static constexpr int KT = 9, NTH = NW * 64, TH = NW * RW, NT = BN / 16;
+  static constexpr int IH = TH + 2, IW = 18, IWP = 20;
+  static constexpr int CH = (CIN + 31) / 32;
+  static constexpr int VCL = CIN - 32 * (CH - 1);
+  static constexpr int TPKL = VCL <= 8 ? 4 : (VCL <= 16 ? 2 : 1);
+  static constexpr int ROWSL = (KT + TPKL - 1) / TPKL;
+  static constexpr int NST = (CH - 1) * KT + ROWSL;         // K steps (stages) per tile
+  static constexpr int NSLF = 4, NSLL = TPKL == 1 ? 4 : 4 / TPKL;   // 8-channel slots staged per chunk
+  static constexpr int PPF = (IH * IW * NSLF + NTH - 1) / NTH;      // image pieces per thread, full chunk
+  static constexpr int PPL = (IH * IW * NSLL + NTH - 1) / NTH;      // ... last chunk
+  static constexpr int PPM = PPF > PPL ? PPF : PPL;
+  static constexpr int IMG = IH * IWP * 32;                 // halves per image (hi or lo)
+  static constexpr int WST = BN * 32;                       // halves per weight stage (hi or lo)
+  static constexpr int NDMA = 2 * BN / 16;                  // 1-KiB LDS-DMA pieces per stage
+  static constexpr int DPW = (NDMA + NW - 1) / NW;          // ... per wave (every wave issues DPW)
+  // LDS (halves): [2 image buffers][hi, lo][IMG] | [3 weight slots][hi, lo][WST] | DMA sink 512 | consts
+  static constexpr int L_W = 4 * IMG;
+  static constexpr int L_SINK = L_W + 6 * WST;
+  static constexpr int L_C = L_SINK + 512;
+  static constexpr size_t lds(int cout) { return (size_t)L_C * 2 + (size_t)2 * cout * 4; }
+  // vector-memory instructions per thread: image chunk loads, tile loads (res, res2), epilogue stores
+  static constexpr int NIMG = 2 * PPM;
+  static constexpr int NTILE = (R2 ? 2 : 1) * RW * NT;
+  static constexpr int NSTORE = RW * NT;
+};
+
+// stage s of a tile -> (chunk, row of the chunk)
+template <int KT, int CH>
+__host__ __device__ constexpr int st_chunk(int s) { return s < (CH - 1) * KT ? s / KT : CH - 1; }
+template <int KT, int CH>
+__host__ __device__ constexpr int st_row(int s) { return s - st_chunk<KT, CH>(s) * KT; }
+
+template <int CIN, int BN, int RW, int NW, bool R2>
+__global__ void __launch_bounds__(NW * 64) xconv3_kernel(XP p) {
+  typedef XG<CIN, BN, RW, NW, R2> G;
+  constexpr int NTH = G::NTH, NT = G::NT, IH = G::IH, IW = G::IW, IWP = G::IWP, IMG = G::IMG;
+  constexpr int WST = G::WST, CH = G::CH, KT = G::KT, TPKL = G::TPKL, ROWSL = G::ROWSL, NST = G::NST;
+  constexpr int NDMA = G::NDMA, DPW = G::DPW, PPF = G::PPF, PPL = G::PPL, PPM = G::PPM;
+  static_assert(NST >= 3, "a tile needs at least three stages");
+  extern __shared__ __align__(16) unsigned char smem[];
+  uint16_t *const L = reinterpret_cast<uint16_t *>(smem);
+  float *const Lc = reinterpret_cast<float *>(smem + (size_t)G::L_C * 2);
+
+  const int tid = threadIdx.x;
+  const int wave = tid >> 6, lane = tid & 63;
+  const int col = lane & 15, hi = lane >> 4;
+  const int GR = gridDim.x;
+  int g = blockIdx.x;
+  if ((GR & 7) == 0) g = (g & 7) * (GR >> 3) + (g >> 3);   // consecutive tiles on one XCD
+  if (g >= p.ntiles) return;
+
+  // bias / scale of every output channel, once
+  for (int i = tid; i < p.cout; i += NTH) {
+    Lc[i] = p.bias ? p.bias[i] : 0.f;
+    Lc[p.cout + i] = p.scale ? p.scale[i] : 1.f;
+  }
+
+  // ---- image piece plans (per thread, constant).  Piece u of a chunk with
+  // NS staged 8-channel slots = (halo row iy, halo column ix, slot): its
+  // element offset from the tile's first halo pixel (prel), its LDS half
+  // offset (lofs), its halo position (ipix: iy << 8 | ix, -1 past the plan)
+  constexpr int NTOTF = IH * IW * 4, NTOTL = IH * IW * G::NSLL;
+  int fprel[PPF], fofs[PPF], fpix[PPF], lprel[PPL], lofs[PPL], lpix[PPL];
+#pragma unroll
+  for (int u = 0; u < PPF; ++u) {
+    const int it = tid + u * NTH;
+    const int slot = it & 3, pix = it >> 2, iy = pix / IW, ix = pix - iy * IW;
+    fpix[u] = it < NTOTF ? (iy << 8) | ix : -1;
+    fofs[u] = swzx(iy * IWP + ix, ix, slot);
+    fprel[u] = (iy * p.W + ix) * p.xcs + slot * 8;
+  }
+#pragma unroll
+  for (int u = 0; u < PPL; ++u) {
+    constexpr int NS = G::NSLL;
+    const int it = tid + u * NTH;
+    const int slot = it % NS, pix = it / NS, iy = pix / IW, ix = pix - iy * IW;
+    lpix[u] = it < NTOTL ? (iy << 8) | ix : -1;
+    lofs[u] = swzx(iy * IWP + ix, ix, slot);
+    lprel[u] = (iy * p.W + ix) * p.xcs + slot * 8;
+  }
+  float pf[PPM][8];   // image pieces in flight (one chunk)
+
+  struct TI {
+    int oy0, ox0, n0;
+  };
+  auto tile_of = [&](int t) {
+    const int nb = t % p.nblk, sp = t / p.nblk;
+    const int ty = sp / p.tiles_x;
+    TI r;
+    r.n0 = nb * BN;
+    r.oy0 = ty * G::TH;
+    r.ox0 = (sp - ty * p.tiles_x) * 16;
+    return r;
+  };
+
+  // registers <- global: the input pieces of chunk c of a tile.  Every load is
+  // issued (halo outside the image and pieces past the plan read zeros
+  // through out-of-range offsets); tiles whose halo lies inside the image
+  // skip the per-piece bounds tests
+  auto load_img = [&](const TI &ti, auto C_) {
+    constexpr int c = decltype(C_)::value;
+    constexpr bool last = c == CH - 1;
+    constexpr int PP = last ? PPL : PPF, NTOT = last ? NTOTL : NTOTF;
+    const int iy0 = ti.oy0 - 1, ix0 = ti.ox0 - 1;
+    const int rb = iy0 > 0 ? iy0 : 0;
+    const int64_t eb = (int64_t)rb * p.W * p.xcs + p.xco + c * 32;
+    int64_t nrec = ((int64_t)p.H * p.W * p.xcs - eb) * 4;
+    if (nrec > 0x7fff0000) nrec = 0x7fff0000;
+    const __amdgpu_buffer_rsrc_t xr =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(p.x + eb), (short)0, (int)nrec, 0x00020000);
+    const int toff = ((iy0 - rb) * p.W + ix0) * p.xcs;
+    const bool inner = iy0 >= 0 && ix0 >= 0 && iy0 + IH <= p.H && ix0 + IW <= p.W;
+#pragma unroll
+    for (int u = 0; u < PPM; ++u) {
+      int o = 0x7fffffe0;
+      if (u < PP) {
+        const int pq = last ? lpix[u < PPL ? u : 0] : fpix[u < PPF ? u : 0];
+        const int pr = last ? lprel[u < PPL ? u : 0] : fprel[u < PPF ? u : 0];
+        o = (toff + pr) * 4;
+        if (!inner) {
+          const int gy = iy0 + (pq >> 8), gx = ix0 + (pq & 255);
+          if (!((unsigned)gy < (unsigned)p.H && (unsigned)gx < (unsigned)p.W)) o = 0x7fffffe0;
+        }
+        if ((u + 1) * NTH > NTOT && pq < 0) o = 0x7fffffe0;
+      }
+      const f32x4 a = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, o, 0, 0));
+      const f32x4 b = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, o + 16, 0, 0));
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        pf[u][j] = a[j];
+        pf[u][4 + j] = b[j];
+      }
+    }
+  };
+  // LDS image buffer ib <- registers, split (ResBlock's leaky ReLU first:
+  // lrelu(v) = max(v, slope v) for 0 <= slope <= 1)
+  auto publish = [&](int ib, auto C_) {
+    constexpr int c = decltype(C_)::value;
+    constexpr bool last = c == CH - 1;
+    constexpr int PP = last ? PPL : PPF, NTOT = last ? NTOTL : NTOTF;
+    uint16_t *const Lh = L + ib * 2 * IMG;
+    if (p.in_lrelu) {
+#pragma unroll
+      for (int u = 0; u < PP; ++u)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) pf[u][j] = fmaxf(pf[u][j], pf[u][j] * p.in_slope);
+    }
+#pragma unroll
+    for (int u = 0; u < PP; ++u) {
+      u32x4_t h, l;
+      split8(pf[u], h, l);
+      const int o = last ? lofs[u] : fofs[u];
+      const bool ok = (u + 1) * NTH <= NTOT || (last ? lpix[u] : fpix[u]) >= 0;
+      if (ok) {
+        *reinterpret_cast<u32x4_t *>(Lh + o) = h;
+        *reinterpret_cast<u32x4_t *>(Lh + IMG + o) = l;
+      }
+    }
+  };
+
+  // LDS-DMA of the weights of stage s (n-block n0) into slot ws: 16 rows of
+  // 64 bytes per instruction; lane i writes physical slot i % 4 of row i / 4,
+  // so it reads the logical slot the swizzle puts there (rows past cout:
+  // zeros).  Every wave issues DPW instructions (the surplus into a sink).
+  // The lane's part of the source offset is fixed: dlane[d]
+  const __amdgpu_buffer_rsrc_t wr =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t *>(p.w), (short)0, p.wbytes, 0x00020000);
+  int dlane[DPW], drow[DPW];
+#pragma unroll
+  for (int d = 0; d < DPW; ++d) {
+    const int i = wave + NW * d;
+    const int hl = i >= NDMA / 2, k = hl ? i - NDMA / 2 : i;
+    const int R = k * 16 + (lane >> 2);
+    const int ls = (lane & 3) ^ ((0x1320 >> (((R >> 2) & 3) << 2)) & 3);
+    dlane[d] = (R * 32 + ls * 8) * 2;
+    drow[d] = R;
+  }
+  auto dma_w = [&](int n0, auto s_, int ws) {
+    constexpr int s = decltype(s_)::value;
+    constexpr int c = st_chunk<KT, CH>(s), rr = st_row<KT, CH>(s);
+    constexpr int rows = c == CH - 1 ? ROWSL : KT;
+    const int nleft = p.cout - n0;
+#pragma unroll
+    for (int d = 0; d < DPW; ++d) {
+      const int i = wave + NW * d;   // wave-uniform
+      const int hl = i >= NDMA / 2, k = hl ? i - NDMA / 2 : i;
+      const int ub = (int)(((int64_t)c * p.wchunk + (hl ? (int64_t)rows * p.cout * 32 : 0) +
+                            ((int64_t)rr * p.cout + n0) * 32) * 2);
+      int voff = ub + dlane[d];
+      if (!(i < NDMA && drow[d] < nleft)) voff = 0x7ffffff0;
+      uint16_t *dst = i < NDMA ? L + G::L_W + ws * 2 * WST + hl * WST + k * 512 : L + G::L_SINK;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(wr, (__attribute__((address_space(3))) void *)dst, 16, voff, 0, 0, 0);
+    }
+  };
+
+  // per-lane operand offsets (halves): weights (row j * 16 + col, slot hi)
+  const int aoff = swz(col, hi);
+  // image, one tap per K step: pixel (wave rows + dy, col + dx), slot hi
+  int bo1[3], bo2[3];
+#pragma unroll
+  for (int dx = 0; dx < 3; ++dx) {
+    const int x = col + dx;
+    bo1[dx] = swzx(wave * RW * IWP + x, x, hi);
+    // packed taps: slot hi % (4 / TPKL)
+    constexpr int spt = 4 / TPKL;
+    bo2[dx] = swzx(wave * RW * IWP + x, x, hi % spt);
+  }
+  const int sub = hi / (4 / TPKL);
+
+  f16x8 oa[2][NT][2], ob[2][RW][2];   // [set][frag][hi, lo]
+  // LDS -> registers: the fragments of stage s (image buffer ib, weight slot ws) into set S
+  auto read_ops = [&](auto S_, auto s_, int ib, int ws) {
+    constexpr int S = decltype(S_)::value;
+    constexpr int s = decltype(s_)::value;
+    constexpr int c = st_chunk<KT, CH>(s), rr = st_row<KT, CH>(s);
+    constexpr int tpk = c == CH - 1 ? TPKL : 1;
+    const uint16_t *Lw = L + G::L_W + ws * 2 * WST + aoff;
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      oa[S][j][0] = *reinterpret_cast<const f16x8 *>(Lw + j * 512);
+      oa[S][j][1] = *reinterpret_cast<const f16x8 *>(Lw + WST + j * 512);
+    }
+    const uint16_t *Li = L + ib * 2 * IMG;
+    if constexpr (tpk == 1) {
+      constexpr int dy = rr / 3, dx = rr % 3;
+#pragma unroll
+      for (int r = 0; r < RW; ++r) {
+        const int o = bo1[dx] + (r + dy) * IWP * 32;
+        ob[S][r][0] = *reinterpret_cast<const f16x8 *>(Li + o);
+        ob[S][r][1] = *reinterpret_cast<const f16x8 *>(Li + IMG + o);
+      }
+    } else {
+      // lane group hi reads tap tpk * rr + sub (a tap past the kernel has
+      // zero weights: any finite data, tap 0)
+      constexpr int ta = tpk * rr, tb = tpk * rr + 1;
+      constexpr int ta_ = ta < KT ? ta : 0, tb_ = tb < KT ? tb : 0;
+      static_assert(tpk == 2, "4-tap packing (<= 8-channel chunks) is not instantiated");
+      const int oA = bo2[ta_ % 3] + (ta_ / 3) * IWP * 32;
+      const int oB = bo2[tb_ % 3] + (tb_ / 3) * IWP * 32;
+      const int o0 = sub ? oB : oA;
+#pragma unroll
+      for (int r = 0; r < RW; ++r) {
+        const int o = o0 + r * IWP * 32;
+        ob[S][r][0] = *reinterpret_cast<const f16x8 *>(Li + o);
+        ob[S][r][1] = *reinterpret_cast<const f16x8 *>(Li + IMG + o);
+      }
+    }
+  };
+
+  f32x4 am[RW][NT], ac[RW][NT];
+  auto mfmas = [&](auto S_) {
+    constexpr int S = decltype(S_)::value;
+#pragma unroll
+    for (int r = 0; r < RW; ++r)
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+        am[r][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(oa[S][j][0], ob[S][r][0], am[r][j], 0, 0, 0);
+        ac[r][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(oa[S][j][0], ob[S][r][1], ac[r][j], 0, 0, 0);
+        ac[r][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(oa[S][j][1], ob[S][r][0], ac[r][j], 0, 0, 0);
+      }
+  };
+
+  // the lane's output pieces: pixel (row wave * RW + r, column col), channels
+  // n0 + 16 j + 4 hi .. + 3; offsets in elements from the tile's first output
+  // pixel.  Full tiles (every piece inside the output) skip the tests
+  auto piece_ok = [&](const TI &ti, int r, int j) {
+    return ti.oy0 + wave * RW + r < p.Ho && ti.ox0 + col < p.Wo && ti.n0 + j * 16 + hi * 4 < p.cout;
+  };
+  auto full_tile = [&](const TI &ti) {
+    return ti.oy0 + G::TH <= p.Ho && ti.ox0 + 16 <= p.Wo && ti.n0 + BN <= p.cout;
+  };
+  // tile-level register loads: residual and second residual of the lane's
+  // output pieces (always issued; zeros when absent or outside the output)
+  f32x4 rv1[RW][NT], rv2[R2 ? RW : 1][NT];
+  auto load_res = [&](const TI &ti) {
+    const int64_t rowb = (int64_t)ti.oy0 * p.Wo;
+    const int nr1 = p.has_res ? 0x7fff0000 : 0;
+    const __amdgpu_buffer_rsrc_t r1 = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float *>(p.has_res ? p.res + rowb * p.rcs + p.rco : p.x), (short)0, nr1, 0x00020000);
+    __amdgpu_buffer_rsrc_t r2 = r1;
+    if constexpr (R2)
+      r2 = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(p.res2 + rowb * p.r2cs + p.r2co), (short)0,
+                                             0x7fff0000, 0x00020000);
+    const bool full = full_tile(ti);
+    const int px = wave * RW * p.Wo + ti.ox0 + col, n = ti.n0 + hi * 4;
+#pragma unroll
+    for (int r = 0; r < RW; ++r)
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+        const bool ok = full || piece_ok(ti, r, j);
+        const int o1 = ok ? ((px + r * p.Wo) * p.rcs + n + j * 16) * 4 : 0x7ffffff0;
+        rv1[r][j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r1, o1, 0, 0));
+        if constexpr (R2) {
+          const int o2 = ok ? ((px + r * p.Wo) * p.r2cs + n + j * 16) * 4 : 0x7ffffff0;
+          rv2[r][j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r2, o2, 0, 0));
+        }
+      }
+  };
+  // out = scale * (res2 + (res + act((am + 2^-11 ac) + bias))), sconv's order
+  // (act: none, or leaky ReLU as max(v, slope v) for 0 <= slope <= 1)
+  auto epilogue = [&](const TI &ti) {
+    const __amdgpu_buffer_rsrc_t yr = __builtin_amdgcn_make_buffer_rsrc(
+        p.y + (int64_t)ti.oy0 * p.Wo * p.ycs + p.yco, (short)0, 0x7fff0000, 0x00020000);
+    const bool full = full_tile(ti);
+    const int px = wave * RW * p.Wo + ti.ox0 + col, n = ti.n0 + hi * 4;
+    f32x4 v[RW][NT];
+#pragma unroll
+    for (int r = 0; r < RW; ++r)
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+        const int nc = n + j * 16 < p.cout ? n + j * 16 : 0;
+        const float4 bb = *reinterpret_cast<const float4 *>(Lc + nc);
+        v[r][j][0] = (am[r][j][0] + ac[r][j][0] * kLoInv) + bb.x;
+        v[r][j][1] = (am[r][j][1] + ac[r][j][1] * kLoInv) + bb.y;
+        v[r][j][2] = (am[r][j][2] + ac[r][j][2] * kLoInv) + bb.z;
+        v[r][j][3] = (am[r][j][3] + ac[r][j][3] * kLoInv) + bb.w;
+      }
+    if (p.act == DCVC_ACT_LRELU) {
+#pragma unroll
+      for (int r = 0; r < RW; ++r)
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[r][j][e] = fmaxf(v[r][j][e], v[r][j][e] * p.slope);
+    }
+    if (p.has_res) {
+#pragma unroll
+      for (int r = 0; r < RW; ++r)
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[r][j][e] = rv1[r][j][e] + v[r][j][e];
+    }
+    if constexpr (R2) {
+#pragma unroll
+      for (int r = 0; r < RW; ++r)
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[r][j][e] = rv2[r][j][e] + v[r][j][e];
+    }
+    if (p.scale) {
+#pragma unroll
+      for (int r = 0; r < RW; ++r)
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+          const int nc = n + j * 16 < p.cout ? n + j * 16 : 0;
+          const float4 sc = *reinterpret_cast<const float4 *>(Lc + p.cout + nc);
+          v[r][j][0] *= sc.x;
+          v[r][j][1] *= sc.y;
+          v[r][j][2] *= sc.z;
+          v[r][j][3] *= sc.w;
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < RW; ++r)
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+        const bool ok = full || piece_ok(ti, r, j);
+        const int o = ok ? ((px + r * p.Wo) * p.ycs + n + j * 16) * 4 : 0x7ffffff0;
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, v[r][j]), yr, o, 0, 0);
+      }
+  };
+
+  // ---- prologue: weights of stages 0 and 1, the first chunk's image
+  const int G0 = GR;
+  {
+    const TI t0 = tile_of(g);
+    dma_w(t0.n0, std::integral_constant<int, 0>{}, 0);
+    dma_w(t0.n0, std::integral_constant<int, 1>{}, 1);
+    load_img(t0, std::integral_constant<int, 0>{});
+  }
+  publish(0, std::integral_constant<int, 0>{});   // (waits for its own loads)
+  // stage 0's weights: the younger DMA (stage 1) may stay in flight
+  wait_vm_n_lgkm<DPW>();
+  __syncthreads();
+  read_ops(std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{}, 0, 0);
+
+  int kw = 0;   // weight slot of the current stage (stage counter mod 3)
+  int q = 0;    // image buffer of the current chunk (chunk counter mod 2)
+  for (int t = g; t < p.ntiles; t += G0) {
+    const int tn = t + G0 < p.ntiles ? t + G0 : t;   // the next tile (prefetch target; itself when last)
+    const TI tc = tile_of(t), tx = tile_of(tn);
+#pragma unroll
+    for (int r = 0; r < RW; ++r)
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+        am[r][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        ac[r][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    sfor<NST>([&](auto s_) {
+      constexpr int s = decltype(s_)::value;
+      // register set of stage s; with an odd stage count the last stage
+      // reads the next tile's stage-0 operands into set 0 after its MFMAs
+      constexpr int S = s & 1;
+      constexpr bool late = (NST & 1) && s == NST - 1;
+      constexpr int c = st_chunk<KT, CH>(s), rr = st_row<KT, CH>(s);
+      constexpr int rows = c == CH - 1 ? ROWSL : KT;
+      // stage s: its weights (slot kw) and image (buffer q) are visible, its
+      // operands are in register set S (read during the previous stage)
+      const int ws2 = kw + 2 >= 3 ? kw - 1 : kw + 2;
+      // 1. weights of stage s + 2 (this tile or the next) into slot kw + 2
+      if constexpr (s + 2 < NST) dma_w(tc.n0, std::integral_constant<int, (s + 2) % NST>{}, ws2);
+      else dma_w(tx.n0, std::integral_constant<int, (s + 2) % NST>{}, ws2);
+      // 2. the next chunk's image pieces (first stage of a chunk)
+      if constexpr (rr == 0) {
+        if constexpr (c + 1 < CH) load_img(tc, std::integral_constant<int, (c + 1 < CH ? c + 1 : 0)>{});
+        else load_img(tx, std::integral_constant<int, 0>{});
+      }
+      // 3. the tile's residuals
+      if constexpr (s == 0) load_res(tc);
+      // 4. operands of stage s + 1 into the other register set (the next
+      // stage's weights landed and were published one barrier ago)
+      const int ws1 = kw + 1 >= 3 ? kw - 2 : kw + 1;
+      constexpr int s1 = s + 1 < NST ? s + 1 : 0;
+      constexpr int c1 = st_chunk<KT, CH>(s1);
+      const int ib1 = (s + 1 < NST ? (c1 == c ? q : q ^ 1) : q ^ 1);
+      if constexpr (!late)
+        read_ops(std::integral_constant<int, S ^ 1>{}, std::integral_constant<int, s1>{}, ib1, ws1);
+      // 5. MFMAs of stage s
+      mfmas(std::integral_constant<int, S>{});
+      if constexpr (late)
+        read_ops(std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{}, ib1, ws1);
+      // 6. the next chunk's image into the other buffer (second-to-last stage
+      // of a chunk: visible at the last stage, whose operand reads need it)
+      if constexpr (rr == rows - 2) {
+        if constexpr (c + 1 < CH) publish(q ^ 1, std::integral_constant<int, (c + 1 < CH ? c + 1 : 0)>{});
+        else publish(q ^ 1, std::integral_constant<int, 0>{});
+      }
+      // 7. epilogue
+      if constexpr (s == NST - 1) epilogue(tc);
+      // end of stage: stage s + 1's weights (the DMA issued one stage before
+      // this one) must have landed; every vector-memory operation issued
+      // after it may stay in flight: the previous stage's after its DMA, and
+      // all of this stage's
+      {
+        constexpr int sp = s == 0 ? NST - 1 : s - 1;
+        constexpr int pv = (st_row<KT, CH>(sp) == 0 ? G::NIMG : 0) + (sp == 0 ? G::NTILE : 0) +
+                           (sp == NST - 1 ? G::NSTORE : 0);
+        constexpr int here = DPW + (rr == 0 ? G::NIMG : 0) + (s == 0 ? G::NTILE : 0) + (s == NST - 1 ? G::NSTORE : 0);
+        constexpr int N = pv + here;
+        static_assert(N < 64, "too many vector-memory operations in flight for vmcnt");
+        wait_vm_n_lgkm<N>();
+      }
+      raw_barrier();
+      if constexpr (rr == rows - 1) q ^= 1;
+      kw = kw + 1 >= 3 ? 0 : kw + 1;
+    });
+  }
+  wait_vm_lgkm();   // no LDS-DMA left in flight when the workgroup exits
+}
+
+int g_cus = 0;
+int g_enable = 1;   // dcvc_set_option("xconv", 0): route every split conv to sconv.hip
+int g_nw = 8;       // dcvc_set_option("xconv_waves", 4 | 8)
+
+template <int CIN, int BN, int RW, int NW, bool R2>
+int launch(XP p, hipStream_t st) {
+  typedef XG<CIN, BN, RW, NW, R2> G;
+  const size_t lds = G::lds(p.cout);
+  if (lds > 160 * 1024) return DCVC_HIP_EUNSUPPORTED;
+  p.tiles_x = (p.Wo + 15) / 16;
+  const int tiles_y = (p.Ho + G::TH - 1) / G::TH;
+  p.nblk = (p.cout + BN - 1) / BN;
+  const int64_t nt = (int64_t)p.tiles_x * tiles_y * p.nblk;
+  if (nt <= 0) return DCVC_HIP_OK;
+  if (nt > 0x7fffffff) return DCVC_HIP_EINVAL;
+  p.ntiles = (int)nt;
+  if (g_cus <= 0) {
+    int dev = 0;
+    hipDeviceProp_t prop;
+    if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess)
+      return DCVC_HIP_ELAUNCH;
+    g_cus = prop.multiProcessorCount;
+  }
+  int64_t grid = g_cus;
+  if (grid > nt) grid = nt;
+  auto kern = xconv3_kernel<CIN, BN, RW, NW, R2>;
+  dcvc_note_kernel("xconv3_kernel<%d, %d, %d, %d, %s>@%lld", CIN, BN, RW, NW, bname(R2), (long long)grid * NW * 64);
+  dcvc_ensure_lds(reinterpret_cast<const void *>(kern), 160 * 1024);
+  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(NW * 64), lds, st, p);
+  DCVC_LAUNCH_CHECK();
+  return DCVC_HIP_OK;
+}
+
+template <int CIN, int BN, bool R2>
+int pick_nw(XP p, hipStream_t st) {
+  if (g_nw == 4) return launch<CIN, BN, 4, 4, R2>(p, st);
+  return launch<CIN, BN, 2, 8, R2>(p, st);
+}
+template <int CIN, int BN>
+int pick_r2(XP p, hipStream_t st) {
+  return p.has_res2 ? pick_nw<CIN, BN, true>(p, st) : pick_nw<CIN, BN, false>(p, st);
+}
+
+template <int CIN>
+int pick_bn(XP p, hipStream_t st) {
+  if (p.cout % 48 == 0 && p.cout <= 48) return pick_r2<CIN, 48>(p, st);
+  if (p.cout % 64 == 0) return pick_r2<CIN, 64>(p, st);
+  if (p.cout % 48 == 0) return pick_r2<CIN, 48>(p, st);
+  if (p.cout % 32 == 0) return pick_r2<CIN, 32>(p, st);
+  return DCVC_HIP_EUNSUPPORTED;
+}
+
+}  // namespace
+
+extern "C" void dcvc_internal_xconv_enable(int v) { g_enable = v; }
+extern "C" void dcvc_internal_sconv_dbg(int v);
+extern "C" void dcvc_internal_sconv_rw(int v);
+
+// the split-precision kernels' A/B and timing-ablation options (dcvc_set_option)
+extern "C" int dcvc_internal_set_option_split(const char *name, int value) {
+  if (std::strcmp(name, "sconv_dbg") == 0) dcvc_internal_sconv_dbg(value);
+  else if (std::strcmp(name, "sconv_rw") == 0) dcvc_internal_sconv_rw(value);
+  else return DCVC_HIP_EINVAL;
+  return DCVC_HIP_OK;
+}
+extern "C" void dcvc_internal_xconv_waves(int v) { g_nw = v; }
+
+// 3x3 stride-1 f16x3 convolutions with fp32 views (dcvc_internal_sconv calls
+// this first).  DCVC_HIP_EUNSUPPORTED: a shape / view without an
+// instantiation, left to sconv.hip.
+extern "C" int dcvc_internal_xconv(const dcvc_conv_args *a, void *stream) {
+  if (!g_enable) return DCVC_HIP_EUNSUPPORTED;
+  if (a->kh != 3 || a->kw != 3 || a->stride != 1 || a->pad != 1 || a->shuffle) return DCVC_HIP_EUNSUPPORTED;
+  if (a->in_op != DCVC_IN_NONE && a->in_op != DCVC_IN_LRELU) return DCVC_HIP_EUNSUPPORTED;
+  if (a->x.dtype != DCVC_F32 || a->y.dtype != DCVC_F32) return DCVC_HIP_EUNSUPPORTED;
+  // leaky ReLUs are computed as max(v, slope v): exact for 0 <= slope <= 1
+  if (a->act != DCVC_ACT_NONE && !(a->act == DCVC_ACT_LRELU && a->slope >= 0.f && a->slope <= 1.f))
+    return DCVC_HIP_EUNSUPPORTED;
+  if (a->in_op == DCVC_IN_LRELU && !(a->in_slope >= 0.f && a->in_slope <= 1.f)) return DCVC_HIP_EUNSUPPORTED;
+  XP p{};
+  p.x = reinterpret_cast<const float *>(a->x.ptr);
+  p.H = a->x.H;
+  p.W = a->x.W;
+  p.xcs = a->x.cstride;
+  p.xco = a->x.coff;
+  p.w = reinterpret_cast<const uint16_t *>(a->w);
+  p.y = reinterpret_cast<float *>(a->y.ptr);
+  p.Ho = a->x.H;
+  p.Wo = a->x.W;
+  p.ycs = a->y.cstride;
+  p.yco = a->y.coff;
+  p.cout = a->cout;
+  p.in_lrelu = a->in_op == DCVC_IN_LRELU;
+  p.in_slope = a->in_slope;
+  p.act = a->act;
+  p.slope = a->slope;
+  p.bias = a->bias;
+  p.scale = a->scale;
+  if (a->y.W != p.Wo || a->y.H != p.Ho) return DCVC_HIP_EUNSUPPORTED;
+  // 16-byte pieces everywhere: input slots of 8 channels, output / residual pieces of 4
+  bool ok = a->cin % 8 == 0 && p.xcs % 4 == 0 && p.xco % 4 == 0 && (uintptr_t)p.x % 16 == 0;
+  ok = ok && a->cout % 4 == 0 && p.ycs % 4 == 0 && p.yco % 4 == 0 && (uintptr_t)p.y % 16 == 0;
+  if (a->res.ptr) {
+    p.res = reinterpret_cast<const float *>(a->res.ptr);
+    p.rcs = a->res.cstride;
+    p.rco = a->res.coff;
+    p.has_res = 1;
+    ok = ok && a->res.dtype == DCVC_F32 && p.rcs % 4 == 0 && p.rco % 4 == 0 && (uintptr_t)p.res % 16 == 0;
+  }
+  if (a->res2.ptr) {
+    p.res2 = reinterpret_cast<const float *>(a->res2.ptr);
+    p.r2cs = a->res2.cstride;
+    p.r2co = a->res2.coff;
+    p.has_res2 = 1;
+    ok = ok && a->res2.dtype == DCVC_F32 && p.r2cs % 4 == 0 && p.r2co % 4 == 0 && (uintptr_t)p.res2 % 16 == 0;
+  }
+  if (!ok) return DCVC_HIP_EUNSUPPORTED;
+  // per-tile buffer offsets stay below 2^31 bytes
+  if ((int64_t)16 * p.Wo * std::max(p.ycs, std::max(p.rcs, p.r2cs)) * 4 >= ((int64_t)1 << 30))
+    return DCVC_HIP_EUNSUPPORTED;
+  const int nch = (a->cin + 31) / 32;
+  const int vc = a->cin - 32 * (nch - 1);
+  const int tpkl = vc <= 8 ? 4 : vc <= 16 ? 2 : 1;
+  p.wchunk = (int64_t)2 * 9 * a->cout * 32;
+  {
+    const int rl = (9 + tpkl - 1) / tpkl;
+    const int64_t wb = ((int64_t)(nch - 1) * p.wchunk + (int64_t)2 * rl * a->cout * 32) * 2;
+    if (wb >= ((int64_t)1 << 31) - 64) return DCVC_HIP_EUNSUPPORTED;
+    p.wbytes = (int)wb;
+  }
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+#ifdef XCONV_ISA_PROBE
+  return pick_bn<48>(p, st);   // (ISA inspection builds: one channel count)
+#else
+  switch (a->cin) {
+    case 32: return pick_bn<32>(p, st);
+    case 48: return pick_bn<48>(p, st);
+    case 64: return pick_bn<64>(p, st);
+    case 80: return pick_bn<80>(p, st);
+    case 96: return pick_bn<96>(p, st);
+    case 128: return pick_bn<128>(p, st);
+    default: return DCVC_HIP_EUNSUPPORTED;
+  }
+#endif
+}

@@ -353,12 +353,42 @@ def four_part_masks(h, w):
     return _MASKS[key]
 
 
-def _masked(y, scales, means, mask):
-    """process_with_mask (common_model.py:92-100)."""
+class Forcer:
+    """Test instrumentation (tests/parity.py, strict bar): replays another
+    coder's symbols at the oracle's rounding ties.  ``syms[c]`` holds the
+    symbols of coder call c (stream order, flattened NCHW); wherever the
+    oracle's pre-rounding value lies within ``eps`` of a half-integer and its
+    rounded symbol differs from ``syms[c]``, the oracle takes ``syms[c]``, so
+    every later step of the frame runs on the same y_hat as that coder.  A
+    difference away from a tie is left in place (the comparison then reports
+    it as unexplained)."""
+
+    def __init__(self, syms, eps):
+        self.syms = syms
+        self.eps = eps
+        self.forced = 0
+
+    def apply(self, call, pre, q, mask=None):
+        if self.syms is None or self.syms[call] is None:
+            return q
+        P = torch.as_tensor(np.asarray(self.syms[call]).astype(np.float32)).reshape(q.shape)
+        a = pre.double().abs()
+        sel = ((a - torch.floor(a) - 0.5).abs() < self.eps) & (P != q)
+        if mask is not None:
+            sel &= mask.bool()
+        self.forced += int(sel.sum())
+        return torch.where(sel, P, q)
+
+
+def _masked(y, scales, means, mask, force=None):
+    """process_with_mask (common_model.py:92-100); ``force(pre, y_q, mask)``:
+    test instrumentation (Forcer)."""
     s_hat = scales * mask
     m_hat = means * mask
     y_res = (y - m_hat) * mask
     y_q = torch.round(y_res)
+    if force is not None:
+        y_q = force(y_res, y_q, mask)
     return y_res, y_q, y_q + m_hat, s_hat
 
 
@@ -367,11 +397,12 @@ def _masked(y, scales, means, mask):
 STEP_MASK = ((0, 1, 2, 3), (3, 2, 1, 0), (2, 3, 0, 1), (1, 0, 3, 2))
 
 
-def four_part_prior(P, y, common_params, adaptors, spatial, yres_out=None):
+def four_part_prior(P, y, common_params, adaptors, spatial, yres_out=None, force=None, call_base=0):
     """forward_four_part_prior with write=True (common_model.py:142-252).
     Returns (per-step symbols y_q_w_k, per-step scales_w_k, y_q, y_hat, scales_hat).
     ``yres_out`` (a list) receives each step's pre-rounding y - means in the
-    layout of y_q_w_k (test instrumentation: distance to a rounding tie)."""
+    layout of y_q_w_k (test instrumentation: distance to a rounding tie);
+    ``force`` (a Forcer) replays coder call call_base + step's symbols at ties."""
     quant_step, scales, means = common_params.chunk(3, 1)
     _, _, H, W = y.size()
     masks = four_part_masks(H, W)
@@ -387,9 +418,12 @@ def four_part_prior(P, y, common_params, adaptors, spatial, yres_out=None):
             out = spatial(conv(P, adaptors[step - 1], params)).chunk(8, 1)
             sc, me = out[:4], out[4:]
         cur = []
+        fk = None
+        if force is not None:
+            fk = (lambda c: (lambda pre, yq, m: force.apply(c, pre, yq, m)))(call_base + step)
         for q in range(4):
             mk = STEP_MASK[step][q]
-            res[q][mk] = _masked(ys[q], sc[q], me[q], masks[mk])
+            res[q][mk] = _masked(ys[q], sc[q], me[q], masks[mk], fk)
             cur.append(res[q][mk][2])
         cur = torch.cat(cur, dim=1)
         y_hat_so_far = cur if step == 0 else y_hat_so_far + cur
@@ -628,7 +662,7 @@ class DMCOracle:
     _MV_AD = ["mv_y_spatial_prior_adaptor_1", "mv_y_spatial_prior_adaptor_2", "mv_y_spatial_prior_adaptor_3"]
     _Y_AD = ["y_spatial_prior_adaptor_1", "y_spatial_prior_adaptor_2", "y_spatial_prior_adaptor_3"]
 
-    def compress(self, x, dpb, q_in_ckpt, q_index, frame_idx, tap=None, recon=False):
+    def compress(self, x, dpb, q_in_ckpt, q_index, frame_idx, tap=None, recon=False, force=None):
         """compress (video_model.py:425-481) minus the encoder-side
         reconstruction, whose output is unused in write mode.  Returns the
         ordered list of coder calls [(kind, symbols, indexes)] and the dpb.
@@ -638,26 +672,29 @@ class DMCOracle:
         scale indexes ("idx_f", y calls), plus the calls in dependency order
         ("order": mv_z, mv_y steps, z, y steps).  ``recon=True`` also returns
         the decoder-side dpb, built from the encoder's y_hat (the same values
-        decompress() reconstructs from the stream)."""
+        decompress() reconstructs from the stream).  ``force`` (a Forcer over
+        the calls in stream order) replays another coder's symbols at ties."""
         P = self.P
+        fa = force.apply if force is not None else (lambda c, pre, q, m=None: q)
         mv_q_enc, mv_q_dec, y_q_enc, y_q_dec = self.get_q(q_in_ckpt, q_index)
         est_mv = spynet(P, "optic_flow", x, dpb["ref_frame"])
         mv_y = mv_enc(P, "mv_encoder", est_mv, dpb["ref_mv_feature"], mv_q_enc)
         mv_y_pad, ss = pad_for_y(mv_y)
         mv_z = hyper_enc(P, "mv_hyper_prior_encoder", mv_y_pad, False)
-        mv_z_hat = torch.round(mv_z)
+        mv_z_hat = fa(0, mv_z, torch.round(mv_z))
         mv_params = self.mv_prior(mv_z_hat, dpb, ss)
         mv_res, y_res = [], []
         mv_sym, mv_sc, _, mv_y_hat, _ = four_part_prior(P, mv_y, mv_params, self._MV_AD,
-                                                        self.spatial("mv_y_spatial_prior"), mv_res)
+                                                        self.spatial("mv_y_spatial_prior"), mv_res, force, 2)
         mv_hat, mv_feature = mv_dec(P, "mv_decoder", mv_y_hat, mv_q_dec)
         c1, c2, c3 = self.motion_compensation(dpb, mv_hat, frame_idx)
         y = contextual_encoder(P, "contextual_encoder", x, c1, c2, c3, y_q_enc)
         y_pad, ss = pad_for_y(y)
         z = hyper_enc(P, "contextual_hyper_prior_encoder", y_pad, True)
-        z_hat = torch.round(z)
+        z_hat = fa(1, z, torch.round(z))
         params = self.res_prior(z_hat, dpb, c3, ss)
-        y_sym, y_sc, _, y_hat, _ = four_part_prior(P, y, params, self._Y_AD, self.spatial("y_spatial_prior"), y_res)
+        y_sym, y_sc, _, y_hat, _ = four_part_prior(P, y, params, self._Y_AD, self.spatial("y_spatial_prior"), y_res,
+                                                   force, 6)
         calls = [("mvz", mv_z_hat, channel_indexes(mv_z_hat)), ("z", z_hat, channel_indexes(z_hat))]
         for s, sc in zip(mv_sym, mv_sc):
             calls.append(("y", s, build_indexes(sc, self.log_min, self.log_step)))
@@ -811,9 +848,9 @@ class IntraOracle:
 
     _AD = ["y_spatial_prior_adaptor_1", "y_spatial_prior_adaptor_2", "y_spatial_prior_adaptor_3"]
 
-    def compress(self, x, q_in_ckpt, q_index, tap=None, recon=False):
+    def compress(self, x, q_in_ckpt, q_index, tap=None, recon=False, force=None):
         """compress (image_model.py:198-229) without the unused encoder recon;
-        ``tap`` / ``recon`` as in DMCOracle.compress."""
+        ``tap`` / ``recon`` / ``force`` as in DMCOracle.compress."""
         q_enc, q_dec = self.get_q(q_in_ckpt, q_index)
         y = self.enc(x, q_enc)
         y_pad, ss = pad_for_y(y)
@@ -821,10 +858,10 @@ class IntraOracle:
         z = depth_conv_block2(P, "hyper_enc.0", y_pad)
         z = lrelu(conv(P, "hyper_enc.1", z, stride=2))
         z = conv(P, "hyper_enc.3", z, stride=2)
-        z_hat = torch.round(z)
+        z_hat = torch.round(z) if force is None else force.apply(0, z, torch.round(z))
         params = self.prior(z_hat, ss)
         y_res = []
-        sym, sc, _, y_hat, _ = four_part_prior(self.P, y, params, self._AD, self.spatial, y_res)
+        sym, sc, _, y_hat, _ = four_part_prior(self.P, y, params, self._AD, self.spatial, y_res, force, 1)
         calls = [("z", z_hat, channel_indexes(z_hat))]
         for s, c in zip(sym, sc):
             calls.append(("y", s, build_indexes(c, self.log_min, self.log_step)))

@@ -140,19 +140,27 @@ def dual_masks(h, w):
     return m0, torch.ones_like(m0) - m0
 
 
-def _masked(y, scales, means, mask):
-    """process_with_mask (models/common_model.py:92-100)."""
+def _masked(y, scales, means, mask, force=None):
+    """process_with_mask (models/common_model.py:92-100); ``force(pre, y_q,
+    mask)``: test instrumentation (dc_oracle.Forcer)."""
     scales_hat = scales * mask
     means_hat = means * mask
     y_res = (y - means_hat) * mask
     y_q = torch.round(y_res)
+    if force is not None:
+        y_q = force(y_res, y_q, mask)
     return y_res, y_q, y_q + means_hat, scales_hat
 
 
-def dual_prior(P, y, means, scales, quant_step, spatial, write=False, res_out=None):
+def dual_prior(P, y, means, scales, quant_step, spatial, write=False, res_out=None, force=None, call_base=0):
     """forward_dual_prior (models/common_model.py:102-156).  ``res_out`` (a
     list) receives the two coder calls' pre-rounding y - means (test
-    instrumentation, tests/parity.py)."""
+    instrumentation, tests/parity.py); ``force`` (a dc_oracle.Forcer) replays
+    coder calls call_base, call_base + 1 at rounding ties."""
+    f0 = f1 = None
+    if force is not None:
+        f0 = lambda pre, q, m: force.apply(call_base, pre, q, m)       # noqa: E731
+        f1 = lambda pre, q, m: force.apply(call_base + 1, pre, q, m)   # noqa: E731
     _, _, H, W = y.size()
     m0, m1 = dual_masks(H, W)
     quant_step = torch.max(quant_step, torch.ones_like(quant_step) * 0.5)
@@ -160,12 +168,12 @@ def dual_prior(P, y, means, scales, quant_step, spatial, write=False, res_out=No
     y_0, y_1 = y.chunk(2, 1)
     s_0, s_1 = scales.chunk(2, 1)
     mu_0, mu_1 = means.chunk(2, 1)
-    r00, q00, h00, sh00 = _masked(y_0, s_0, mu_0, m0)
-    r11, q11, h11, sh11 = _masked(y_1, s_1, mu_1, m1)
+    r00, q00, h00, sh00 = _masked(y_0, s_0, mu_0, m0, f0)
+    r11, q11, h11, sh11 = _masked(y_1, s_1, mu_1, m1, f0)
     params = torch.cat((h00, h11, means, scales, quant_step), dim=1)
     s_0, mu_0, s_1, mu_1 = spatial(params).chunk(4, 1)
-    r01, q01, h01, sh01 = _masked(y_0, s_0, mu_0, m1)
-    r10, q10, h10, sh10 = _masked(y_1, s_1, mu_1, m0)
+    r01, q01, h01, sh01 = _masked(y_0, s_0, mu_0, m1, f1)
+    r10, q10, h10, sh10 = _masked(y_1, s_1, mu_1, m0, f1)
     y_q = torch.cat((q00 + q01, q11 + q10), dim=1)
     y_hat = torch.cat((h00 + h01, h11 + h10), dim=1)
     scales_hat = torch.cat((sh00 + sh01, sh11 + sh10), dim=1)
@@ -287,7 +295,7 @@ class DMCOracle:
     def spatial(self, prefix):
         return lambda t: seq3(self.P, prefix, t)
 
-    def compress(self, x, dpb, mv_y_q_scale, y_q_scale, tap=None, recon=False):
+    def compress(self, x, dpb, mv_y_q_scale, y_q_scale, tap=None, recon=False, force=None):
         """compress (:263-330): the coder calls [(table, symbols, scales)].
         Test instrumentation: ``tap`` (a dict) receives per call the
         pre-rounding values ("pre"), the pre-truncation scale indexes
@@ -300,20 +308,21 @@ class DMCOracle:
         est_mv = spynet(P, "optic_flow", x, dpb["ref_frame"])
         mv_y = enc_model(P, "mv_encoder", est_mv) / mvq
         mv_z = hyper_enc(P, "mv_hyper_prior_encoder", mv_y)
-        mv_z_hat = torch.round(mv_z)
+        mv_z_hat = torch.round(mv_z) if force is None else force.apply(0, mv_z, torch.round(mv_z))
         mv_q_step, mv_scales, mv_means = self.mv_params(mv_z_hat, dpb["ref_mv_y"], mv_y)
         res = []
         mq0, mq1, ms0, ms1, mv_y_hat = dual_prior(P, mv_y, mv_means, mv_scales, mv_q_step,
-                                                  self.spatial("mv_y_spatial_prior"), write=True, res_out=res)
+                                                  self.spatial("mv_y_spatial_prior"), write=True, res_out=res,
+                                                  force=force, call_base=1)
         mv_y_hat = mv_y_hat * mvq
         mv_hat = dec_model(P, "mv_decoder", mv_y_hat)
         c1, c2, c3 = self.motion_compensation(dpb, mv_hat)
         y = self.contextual_encoder(x, c1, c2, c3) / yq
         z = ctx_hyper_enc(P, y)
-        z_hat = torch.round(z)
+        z_hat = torch.round(z) if force is None else force.apply(3, z, torch.round(z))
         q_step, scales, means = self.y_params(z_hat, c3, dpb["ref_y"], y)
         q0, q1, s0, s1, y_hat = dual_prior(P, y, means, scales, q_step, self.spatial("y_spatial_prior"),
-                                           write=True, res_out=res)
+                                           write=True, res_out=res, force=force, call_base=4)
         calls = [("p_mvz", mv_z_hat, None), ("p_y", mq0, ms0), ("p_y", mq1, ms1), ("p_z", z_hat, None),
                  ("p_y", q0, s0), ("p_y", q1, s1)]
         if tap is not None:
@@ -410,17 +419,17 @@ class IntraOracle:
         P = self.P
         return conv(P, "refine.1", unet(P, "refine.0", dec_model(P, "dec", y_hat)))
 
-    def compress(self, x, q_scale, tap=None, recon=False):
-        """compress (:150-154); ``tap`` / ``recon`` as in DMCOracle.compress."""
+    def compress(self, x, q_scale, tap=None, recon=False, force=None):
+        """compress (:150-154); ``tap`` / ``recon`` / ``force`` as in DMCOracle.compress."""
         P = self.P
         q = lower_bound_q(P, "q_basic", q_scale)
         y = enc_model(P, "enc", x) / q
         z = hyper_enc(P, "hyper_enc", y)
-        z_hat = torch.round(z)
+        z_hat = torch.round(z) if force is None else force.apply(0, z, torch.round(z))
         q_step, scales, means = self._prior(z_hat)
         res = []
         q0, q1, s0, s1, y_hat = dual_prior(P, y, means, scales, q_step, lambda t: seq3(P, "y_spatial_prior", t),
-                                           write=True, res_out=res)
+                                           write=True, res_out=res, force=force, call_base=1)
         calls = [("i_z", z_hat, None), ("i_y", q0, s0), ("i_y", q1, s1)]
         if tap is not None:
             lm, st = self.tab_y[3], self.tab_y[4]

@@ -15,14 +15,20 @@ checked here as:
   * the first symbol that differs, in the order the codec computes them
     (mv_z, mv_y quadtree steps, z, y quadtree steps), must be such a tie.  A
     changed symbol changes y_hat, which every later step and call of the frame
-    reads, so differences after it are a consequence (a "cascade") and are
-    counted, not excused one by one;
+    reads, so differences after it are a consequence (a "cascade");
+  * the cascade is then checked element by element, not excused: the oracle
+    codes the frame again with the product's symbols replayed at its own
+    rounding ties (oracle.dc_oracle.Forcer), so it runs every later step on the
+    product's y_hat.  In that replay every symbol must equal the product's and
+    every index must equal it or sit on a tie of the replay's own values
+    (compare_forced), and the product's reconstruction must lie within PSNR_DB
+    of the replay's, which is the oracle's decode of the product's stream;
   * a frame whose calls all agree has identical bits (the coder is
     deterministic) and its reconstruction within PSNR_DB of the oracle's.
 """
 import numpy as np
 
-TIE_EPS = 2e-3        # distance of an oracle value to the rounding discontinuity
+TIE_EPS = 1e-3        # distance of an oracle value to the rounding discontinuity (largest seen: 4.5e-4)
 PSNR_DB = 1e-4        # BASELINE.json: PSNR delta < 1e-4 dB
 
 
@@ -86,6 +92,47 @@ def compare_frame(prod_calls, oracle_calls, tap):
         out["calls"].append(rec)
     out["identical"] = out["sym_diff"] == 0 and out["idx_diff"] == 0
     return out
+
+
+def compare_forced(prod_calls, oracle_calls, tap, forced):
+    """The replay (module docstring): oracle_calls / tap from the oracle coding
+    the frame with the product's symbols forced at ties (``forced`` of them).
+    Every symbol must now agree; every differing index must be a tie of the
+    replay's own pre-truncation values."""
+    out = {"forced": int(forced), "sym_diff": 0, "idx_diff": 0, "unexplained": [], "max_tie_dist": 0.0}
+    for c in tap["order"]:
+        ps, pi = (np.asarray(a).reshape(-1) for a in prod_calls[c])
+        kind, os_, oi = oracle_calls[c]
+        os_ = np.clip(_np(os_), -30000, 30000).astype(np.int64)
+        oi = _np(oi).astype(np.int64)
+        ds = np.nonzero(ps.astype(np.int64) != os_)[0]
+        di = np.nonzero(pi.astype(np.int64) != oi)[0]
+        out["sym_diff"] += int(ds.size)
+        out["idx_diff"] += int(di.size)
+        if ds.size:
+            d = sym_tie_distance(_np(tap["pre"][c])[ds])
+            out["unexplained"].append({"call": c, "what": "symbol (replay)", "pos": ds[:8].tolist(),
+                                       "dist": d[:8].tolist()})
+        if di.size:
+            d = idx_tie_distance(_np(tap["idx_f"][c])[di]) if tap["idx_f"][c] is not None else np.full(di.size, 1.0)
+            out["max_tie_dist"] = max(out["max_tie_dist"], float(d.max()))
+            bad = di[d >= TIE_EPS]
+            if bad.size:
+                out["unexplained"].append({"call": c, "what": "index (replay)", "pos": bad[:8].tolist(),
+                                           "dist": d[d >= TIE_EPS][:8].tolist()})
+    out["identical"] = out["sym_diff"] == 0 and out["idx_diff"] == 0
+    return out
+
+
+def check_forced(sf, bits, bits_replay, psnr, psnr_replay, name=""):
+    """The replay's bar (compare_forced's dict)."""
+    msg = (f"{name} replay: forced={sf['forced']} dsym={sf['sym_diff']} didx={sf['idx_diff']}, "
+           f"bits {bits} vs replay {bits_replay}, dPSNR={psnr - psnr_replay:.3g} dB, unexplained={sf['unexplained']}")
+    assert not sf["unexplained"], msg
+    if sf["identical"]:
+        assert bits == bits_replay, msg
+    assert abs(psnr - psnr_replay) < PSNR_DB, msg
+    return msg
 
 
 def check_frame(st, bits, bits_oracle, psnr, psnr_oracle, name=""):

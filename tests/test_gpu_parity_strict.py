@@ -18,7 +18,7 @@ import numpy as np
 import pytest
 import torch
 
-from tests.parity import compare_frame, check_frame
+from tests.parity import TIE_EPS, check_forced, check_frame, compare_forced, compare_frame
 
 pytestmark = pytest.mark.gpu
 
@@ -61,14 +61,14 @@ class Pair:
         self.pi.update(force=True)
         self.pp.update(force=True)
 
-    def oracle(self, t, xp, dpb, q, fidx):
+    def oracle(self, t, xp, dpb, q, fidx, force=None):
         tap = {}
         with torch.no_grad():
             if t == 0:
-                calls, xh = self.oi.compress(xp, False, q, tap=tap, recon=True)
+                calls, xh = self.oi.compress(xp, False, q, tap=tap, recon=True, force=force)
                 dpb = {"ref_frame": xh, "ref_feature": None, "ref_mv_feature": None, "ref_y": None, "ref_mv_y": None}
             else:
-                calls, dpb = self.op.compress(xp, dpb, False, q, fidx, tap=tap, recon=True)
+                calls, dpb = self.op.compress(xp, dpb, False, q, fidx, tap=tap, recon=True, force=force)
         pre = "i_" if t == 0 else "p_"
         cc = [(s.clamp(-30000, 30000).to(torch.int16).numpy(), ix.to(torch.int16).numpy(), self.tabs[pre + k])
               for k, s, ix in calls]
@@ -109,7 +109,20 @@ def run_teacher_forced(pair, frames, q, h, w, name):
             p = psnr(rec[:, :, :h, :w], x)
             p_o = psnr(dpb_next["ref_frame"][:, :, :h, :w], x)
             st.update({"t": t, "bits": int(bits), "bits_oracle": int(bits_o), "psnr": p, "psnr_oracle": p_o})
-            stats.append((st, check_frame(st, bits, bits_o, p, p_o, f"{name} t={t}")))
+            msg = check_frame(st, bits, bits_o, p, p_o, f"{name} t={t}")
+            if st["sym_diff"]:
+                # the cascade after a flipped tie, element by element: the
+                # oracle replays the product's symbols at its ties and runs the
+                # rest of the frame on the product's y_hat
+                from oracle.dc_oracle import Forcer
+                fr = Forcer([s for s, _ in enc], TIE_EPS)
+                calls_f, tap_f, bits_f, dpb_f = pair.oracle(t, xp, dpb_o, q, fidx, force=fr)
+                sf = compare_forced(enc, calls_f, tap_f, fr.forced)
+                p_f = psnr(dpb_f["ref_frame"][:, :, :h, :w], x)
+                sf.update({"bits_replay": int(bits_f), "psnr_replay": p_f})
+                st["replay"] = sf
+                msg += "\n" + check_forced(sf, bits, bits_f, p, p_f, f"{name} t={t}")
+            stats.append((st, msg))
             dpb_o = dpb_next
     os.makedirs(OUT, exist_ok=True)
     path = os.path.join(OUT, "parity_strict.json")
@@ -205,16 +218,16 @@ class HemPair(Pair):
         idx = np.concatenate([i.reshape(-1).astype(np.int32) + base[k] for k, _, i in calls])
         return len(self.R.hem_encode(sym, idx, cdfs, sizes, offs))
 
-    def oracle(self, t, xp, dpb, q, fidx):
+    def oracle(self, t, xp, dpb, q, fidx, force=None):
         O = self.O
         qi, qmv, qy = (round(v * 100) / 100 for v in self.q)
         tap = {}
         with torch.no_grad():
             if t == 0:
-                calls, xh = self.oi.compress(xp, qi, tap=tap, recon=True)
+                calls, xh = self.oi.compress(xp, qi, tap=tap, recon=True, force=force)
                 dpb = {"ref_frame": xh, "ref_feature": None, "ref_y": None, "ref_mv_y": None}
             else:
-                calls, dpb = self.op.compress(xp, dpb, qmv, qy, tap=tap, recon=True)
+                calls, dpb = self.op.compress(xp, dpb, qmv, qy, tap=tap, recon=True, force=force)
         net = self.oi if t == 0 else self.op
         out = []
         for kind, sym, sc in calls:

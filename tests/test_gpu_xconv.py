@@ -1,0 +1,127 @@
+"""The static-shape split-fp16 3x3 kernel (xconv.hip) against sconv.hip and fp64.
+
+xconv_kernel computes the same products in the same K order with the same
+epilogue as sconv_kernel, so its output must be bit-identical to sconv's
+(dcvc_set_option("xconv", 0) routes the call to sconv.hip) and within the
+split precision's fp64 bound (4e-6 of the output magnitude, as in
+test_gpu_sconv.py).  The shapes are the 3x3 stride-1 layers of the DC and
+HEM feature-rate stacks (DCVC-DC/src/models/video_net.py:58-76, 129-170,
+video_model.py:89-118, 173-232), at sizes where every workgroup walks many
+tiles (the persistent pipeline: weight ring, image double buffer, next-tile
+prefetch, vmcnt accounting) and at ragged sizes (partial tiles, n-blocks that
+pad cout), with the whole epilogue (in_op leaky ReLU, act, residual, second
+residual, scale) on channel views.
+"""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+TOL = 4e-6
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+def K():
+    from dcvc_amd import hip
+    return hip
+
+
+def rel_err(got, ref):
+    scale = ref.abs().max().item() + 1e-12
+    return (got.double() - ref).abs().max().item() / scale
+
+
+def run(h, cw, x, out, opts, **kw):
+    for k, v in opts.items():
+        h.set_option(k, v)
+    try:
+        h.conv(cw, x, out, **kw)
+        torch.cuda.synchronize()
+        return h.lib().dcvc_last_kernel().decode()
+    finally:
+        for k in opts:
+            h.set_option(k, 1 if k == "xconv" else 8)
+
+
+# cin, cout, H, W, residual, second residual, in_op leaky ReLU
+CASES = [
+    (48, 48, 272, 480, True, False, True),     # ResBlock conv2 shape, many tiles per workgroup
+    (48, 48, 37, 53, False, False, True),      # ragged tiles
+    (48, 48, 96, 130, True, True, False),      # context fusion res_block1_out conv2 (two residuals)
+    (64, 64, 136, 240, True, False, True),
+    (64, 64, 21, 35, True, True, False),
+    (96, 48, 70, 90, False, False, False),     # conv1_out / first_conv (BN = 48, 3 chunks)
+    (80, 48, 40, 66, False, False, False),     # 16-channel last chunk after two full chunks
+    (128, 64, 68, 120, False, False, False),
+    (96, 96, 68, 120, True, False, True),
+    (64, 128, 34, 60, False, False, False),    # two 64-channel n-blocks
+    (64, 96, 17, 31, False, False, False),     # 96 = 2 x 48
+    (32, 48, 33, 47, False, False, False),     # one chunk (odd stage count)
+    (32, 32, 50, 20, True, False, False),
+    (128, 32, 19, 23, False, False, False),
+]
+
+
+@pytest.mark.parametrize("waves", [8, 4])
+@pytest.mark.parametrize("case", CASES)
+def test_xconv_matches_sconv_and_fp64(case, waves):
+    h = K()
+    cin, cout, H, W, res, res2, lrelu = case
+    g = torch.Generator().manual_seed(cin * 7 + cout + H)
+    big = torch.randn(1, cin + 8, H, W, generator=g)
+    big[:, :, ::3] *= 1e-3          # small values: the lo parts go subnormal in fp16
+    x = big[:, 4:4 + cin]
+    w = torch.randn(cout, cin, 3, 3, generator=g) / (cin * 9) ** 0.5
+    b = torch.randn(cout, generator=g) * 0.1
+    r = torch.randn(1, cout, H, W, generator=g) if res else None
+    r2 = torch.randn(1, cout, H, W, generator=g) if res2 else None
+    sc = torch.rand(cout, generator=g) + 0.5
+    xd = F.leaky_relu(x.double(), 0.01) if lrelu else x.double()
+    ref = F.leaky_relu(F.conv2d(xd, w.double(), b.double(), padding=1), 0.1)
+    if res:
+        ref = r.double() + ref
+    if res2:
+        ref = r2.double() + ref
+    ref = ref * sc.double().view(1, -1, 1, 1)
+    cw = h.ConvW(w, b, 1, h.F16X3)
+    xa = h.from_nchw(big, h.F32).ch(4, cin)
+    kw = dict(act=h.ACT_LRELU, slope=0.1, scale=sc.cuda(),
+              in_op=h.IN_LRELU if lrelu else h.IN_NONE, in_slope=0.01,
+              res=h.from_nchw(r, h.F32) if res else None, res2=h.from_nchw(r2, h.F32) if res2 else None)
+    outs = []
+    for opts in ({"xconv": 1, "xconv_waves": waves}, {"xconv": 0}):
+        out = h.empty(H, W, cout + 12, h.F32)
+        out.buf.fill_(7.0)
+        kern = run(h, cw, xa, out.ch(4, cout), opts, **kw)
+        assert kern.startswith("xconv3_kernel" if opts["xconv"] else "sconv_kernel"), kern
+        # nothing written outside the view
+        assert bool((out.buf[:, :, :4] == 7.0).all()) and bool((out.buf[:, :, 4 + cout:] == 7.0).all())
+        outs.append(out.ch(4, cout).nchw().cpu())
+    assert rel_err(outs[0], ref) < TOL
+    assert torch.equal(outs[0], outs[1])
+
+
+def test_xconv_repeatable_under_load():
+    """The same launch twice, and interleaved with another shape's launches on
+    the same stream: identical bits (no stale LDS slot, no DMA race)."""
+    h = K()
+    g = torch.Generator().manual_seed(5)
+    x = h.from_nchw(torch.randn(1, 48, 544, 960, generator=g), h.F32)
+    w = torch.randn(48, 48, 3, 3, generator=g) / (48 * 9) ** 0.5
+    cw = h.ConvW(w, torch.randn(48, generator=g) * 0.1, 1, h.F16X3)
+    cw2 = h.ConvW(torch.randn(64, 48, 3, 3, generator=g) / 20, torch.zeros(64), 1, h.F16X3)
+    y0 = h.conv(cw, x, out_dtype=h.F32)
+    torch.cuda.synchronize()
+    assert h.lib().dcvc_last_kernel().decode().startswith("xconv3_kernel")
+    ref = y0.buf.clone()
+    for _ in range(3):
+        h.conv(cw2, x, out_dtype=h.F32)
+        h.conv(cw, x, y0)
+    torch.cuda.synchronize()
+    assert torch.equal(y0.buf, ref)
