@@ -72,6 +72,9 @@ void dcvc_note_kernel(const char *fmt, ...);
 // under a lock: setting the attribute while another host thread launches the
 // same kernel on another stream (concurrent GOP lanes) is not safe.
 void dcvc_ensure_lds(const void *kern, int bytes);
+// the calling host thread's fp16 range-guard flag of the split kernels
+// (dcvc_split_range_flag; nullptr: guard off), read by their launchers
+int *dcvc_internal_split_flag();
 template <typename T> constexpr const char *tname();
 template <> constexpr const char *tname<float>() { return "float"; }
 template <> constexpr const char *tname<uint16_t>() { return "unsigned short"; }

@@ -528,7 +528,10 @@ static int64_t pack_f16x3(const float *w, int cout, int cin, int kh, int kw, uin
 extern "C" int64_t dcvc_conv_pack_weights(const float *w, int cout, int cin, int kh, int kw,
                                           int compute, void *out) {
   if (!w || cout <= 0 || cin <= 0 || kh <= 0 || kw <= 0) return DCVC_HIP_EINVAL;
-  if (compute == DCVC_F16X3) return pack_f16x3(w, cout, cin, kh, kw, reinterpret_cast<uint16_t *>(out));
+  if (compute == DCVC_F16X3) {
+    if (out && !host_split_range_ok(w, (int64_t)cout * cin * kh * kw)) return DCVC_HIP_EINVAL;
+    return pack_f16x3(w, cout, cin, kh, kw, reinterpret_cast<uint16_t *>(out));
+  }
   if (!out) return DCVC_HIP_EINVAL;
   const int cinp = (cin + kChunk - 1) / kChunk * kChunk;
   const int64_t total = (int64_t)cout * kh * kw * cinp;
@@ -586,6 +589,18 @@ extern "C" int dcvc_internal_set_option_split(const char *name, int value);
 extern "C" int dcvc_internal_xconv(const dcvc_conv_args *a, void *stream);
 extern "C" void dcvc_internal_xconv_enable(int v);
 extern "C" void dcvc_internal_xconv_waves(int v);
+
+// fp16 range guard of the split kernels (split.h SplitRange): one flag per
+// calling host thread (concurrent GOP lanes each launch from their own thread
+// on their own stream)
+namespace {
+thread_local int *t_split_flag = nullptr;
+}
+int *dcvc_internal_split_flag() { return t_split_flag; }
+extern "C" int dcvc_split_range_flag(int *flag) {
+  t_split_flag = flag;
+  return DCVC_HIP_OK;
+}
 
 extern "C" int dcvc_conv2d(const dcvc_conv_args *a, void *stream) {
   if (!a || !a->w || !valid_view(a->x) || !valid_view(a->y)) return DCVC_HIP_EINVAL;

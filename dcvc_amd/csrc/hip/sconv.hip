@@ -78,6 +78,7 @@ struct SP {
   int wbytes;              // bytes of the packed weights
   int dbg;                 // dcvc_set_option("sconv_dbg", mask): timing ablations, wrong results
                            // (1 no MFMA, 2 no image publish, 4 no image loads, 8 no epilogue)
+  int *ovf;               // fp16 range guard (split.h SplitRange)
 };
 
 // RES = false: weights streamed one kernel row (KS taps) of one chunk per
@@ -118,6 +119,7 @@ __device__ __forceinline__ int chunk_rows(int kt, int tpk) { return (kt + tpk - 
 
 template <int KS, int S, int BN, int RW, int NW, bool GATE, bool RES>
 __global__ void __launch_bounds__(NW * 64) sconv_kernel(SP p) {
+  SplitRange rg(p.ovf);
   typedef SG<KS, S, BN, RW, NW, RES> G_;
   constexpr int kNW = NW, kNT = NW * 64;
   constexpr int TH = G_::TH, NT = G_::NT, KT = G_::KT, RG = G_::RG;
@@ -245,6 +247,7 @@ __global__ void __launch_bounds__(NW * 64) sconv_kernel(SP p) {
   // 0 <= slope <= 1, and the ConvFFN2 gate are applied before the split)
   auto publish_one = [&](int u, const float (&v)[8]) {
     u32x4_t h, l;
+    rg.add8(v);
     split8(v, h, l);
     const bool ok = ipix[u] >= 0;
     *reinterpret_cast<u32x4_t *>(ok ? Lih + iofs[u] : Ldummy) = h;
@@ -695,6 +698,7 @@ extern "C" int dcvc_internal_sconv(const dcvc_conv_args *a, void *stream) {
     if (r != DCVC_HIP_EUNSUPPORTED) return r;
   }
   SP p{};
+  p.ovf = dcvc_internal_split_flag();
   p.x = reinterpret_cast<const float *>(a->x.ptr);
   p.H = a->x.H;
   p.W = a->x.W;

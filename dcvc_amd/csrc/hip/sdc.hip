@@ -37,6 +37,7 @@ struct DP {
   const float *b1, *wdw, *bdw, *b2, *ba;
   float slope;
   int tiles_x, ntiles;
+  int *ovf;               // fp16 range guard (split.h SplitRange)
 };
 
 template <int CIN, int COUT, bool ADAPT>
@@ -61,6 +62,7 @@ __device__ __forceinline__ float lrelu(float v, float s) { return fmaxf(v, v * s
 
 template <int CIN, int COUT, bool ADAPT>
 __global__ void __launch_bounds__(kNT) sdc_kernel(DP p) {
+  SplitRange rg(p.ovf);
   typedef DG<CIN, COUT, ADAPT> G_;
   constexpr int KCI = G_::KCI, NTI = G_::NTI, NTO = G_::NTO, CO16 = G_::CO16, CI16 = G_::CI16;
   constexpr int XI = G_::XI, DI = G_::DI, QP = G_::QP, PP = G_::PP;
@@ -167,6 +169,7 @@ __global__ void __launch_bounds__(kNT) sdc_kernel(DP p) {
 #pragma unroll
     for (int u = 0; u < PP; ++u) {
       u32x4_t h, l;
+      rg.add8(pf[u]);
       split8(pf[u], h, l);
       if (pyx[u] >= 0) {
         *reinterpret_cast<u32x4_t *>(Xh + pofs[u]) = h;
@@ -271,6 +274,7 @@ __global__ void __launch_bounds__(kNT) sdc_kernel(DP p) {
         float v[4];
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[e] = a[e] + Lbdw[c + e];
+        rg.add4(v);
         const auto h01 = __builtin_amdgcn_cvt_pkrtz(v[0], v[1]);
         const auto h23 = __builtin_amdgcn_cvt_pkrtz(v[2], v[3]);
         const uint32_t l01 = pk((v[0] - (float)h01[0]) * 2048.f, (v[1] - (float)h01[1]) * 2048.f);
@@ -377,6 +381,9 @@ bool supported(int cin, int cout, bool adapt) {
 extern "C" int64_t dcvc_dc_pack_weights(const float *w1, const float *w2, const float *wa, int cin, int cout,
                                         void *out) {
   if (!w1 || !w2 || cin <= 0 || cout <= 0) return DCVC_HIP_EINVAL;
+  if (out && (!host_split_range_ok(w1, (int64_t)cin * cin) || !host_split_range_ok(w2, (int64_t)cout * cin) ||
+              (wa && !host_split_range_ok(wa, (int64_t)cout * cin))))
+    return DCVC_HIP_EINVAL;
   const int kci = (cin + 31) / 32, ci16 = (cin + 15) / 16 * 16, co16 = (cout + 15) / 16 * 16;
   const int64_t n1 = (int64_t)kci * ci16 * 32, n2 = (int64_t)kci * co16 * 32, na = wa ? n2 : 0;
   const int64_t total = 2 * (n1 + n2 + na);
@@ -415,6 +422,7 @@ extern "C" int dcvc_depth_conv_split(const dcvc_dc_args *a, void *stream) {
     return DCVC_HIP_EUNSUPPORTED;
   if ((int64_t)a->x.H * a->x.W * a->x.cstride * 4 >= ((int64_t)1 << 31) - 64) return DCVC_HIP_EUNSUPPORTED;
   DP p{};
+  p.ovf = dcvc_internal_split_flag();
   p.x = reinterpret_cast<const float *>(a->x.ptr);
   p.H = a->x.H;
   p.W = a->x.W;

@@ -43,6 +43,7 @@ struct FP {
   const float *b1, *b2, *scale;
   float slope;
   int ntiles;
+  int *ovf;               // fp16 range guard (split.h SplitRange)
 };
 
 template <int C, int HS, int NBUF>
@@ -69,6 +70,7 @@ __device__ __forceinline__ float lrelu(float v, float s) { return fmaxf(v, v * s
 
 template <int C, int HS, int NBUF>
 __global__ void __launch_bounds__(kNT) sffn_kernel(FP p) {
+  SplitRange rg(p.ovf);
   typedef FG<C, HS, NBUF> G_;
   constexpr int KC1 = G_::KC1, NT = G_::NT, NH = G_::NH, KC2 = G_::KC2, PP = G_::PP;
   constexpr int W1 = G_::W1, W2 = G_::W2, SLICE = G_::SLICE, XI = G_::XI, HI = G_::HI, NDMA = G_::NDMA;
@@ -118,6 +120,7 @@ __global__ void __launch_bounds__(kNT) sffn_kernel(FP p) {
         const int px = it / QP, q = it - px * QP;
         const int kc = q >> 2, slot = q & 3;
         u32x4_t h, l;
+        rg.add8(pf[u]);
         split8(pf[u], h, l);
         const int o = swz(kc * TP + px, slot);
         *reinterpret_cast<u32x4_t *>(Xh + o) = h;
@@ -214,6 +217,7 @@ __global__ void __launch_bounds__(kNT) sffn_kernel(FP p) {
         v[1] = lrelu((hm[j][1] + hc[j][1] * kLoInv) + bb.y, p.slope);
         v[2] = lrelu((hm[j][2] + hc[j][2] * kLoInv) + bb.z, p.slope);
         v[3] = lrelu((hm[j][3] + hc[j][3] * kLoInv) + bb.w, p.slope);
+        rg.add4(v);
         const auto h01 = __builtin_amdgcn_cvt_pkrtz(v[0], v[1]);
         const auto h23 = __builtin_amdgcn_cvt_pkrtz(v[2], v[3]);
         const uint32_t l01 = pk((v[0] - (float)h01[0]) * 2048.f, (v[1] - (float)h01[1]) * 2048.f);
@@ -320,6 +324,8 @@ extern "C" int dcvc_internal_lffn(const dcvc_ffn_args *a, void *stream);
 // [kc2][n][32], 16-byte slots swizzled by swz()).  out NULL: size query.
 extern "C" int64_t dcvc_ffn_pack_weights(const float *w1, const float *w2, int c, int hidden, void *out) {
   if (!w1 || !w2 || c <= 0 || hidden <= 0) return DCVC_HIP_EINVAL;
+  if (out && (!host_split_range_ok(w1, (int64_t)hidden * c) || !host_split_range_ok(w2, (int64_t)c * hidden)))
+    return DCVC_HIP_EINVAL;
   // the latent widths: MFMA fragments for slffn.hip
   if (dcvc_internal_lffn_supported(c, hidden)) return dcvc_internal_lffn_pack(w1, w2, c, hidden, out);
   const int HS = hs_of(c);
@@ -367,6 +373,7 @@ extern "C" int dcvc_conv_ffn(const dcvc_ffn_args *a, void *stream) {
     return DCVC_HIP_EUNSUPPORTED;
   if (dcvc_internal_lffn_supported(a->c, a->hidden)) return dcvc_internal_lffn(a, stream);   // slffn.hip
   FP p{};
+  p.ovf = dcvc_internal_split_flag();
   p.x = reinterpret_cast<const float *>(a->x.ptr);
   p.npix = a->x.H * a->x.W;
   p.xcs = a->x.cstride;

@@ -53,6 +53,7 @@ struct GP {
   const float *res2;
   int r2cs, r2co;
   int shuffle, W;   // pixel shuffle (x2) on store: the input map's width W
+  int *ovf;               // fp16 range guard (split.h SplitRange)
 };
 
 template <int BN, int PXW, int PD>
@@ -74,6 +75,7 @@ constexpr int kOob = 0x7fffffe0;   // a buffer offset past any num_records: the 
 
 template <int BN, int PXW, int PD>
 __global__ void __launch_bounds__(256) sgemm_kernel(GP p) {
+  SplitRange rg(p.ovf);
   typedef GG<BN, PXW, PD> G_;
   constexpr int NT = G_::NT, BM = G_::BM, NB = G_::NB, WH = G_::WH, SH = G_::SH, DPW = G_::DPW, L = G_::L;
   extern __shared__ __align__(16) unsigned char smem[];
@@ -189,6 +191,7 @@ __global__ void __launch_bounds__(256) sgemm_kernel(GP p) {
         for (int e = 0; e < 8; ++e) v[e] = v[e] >= 0.f ? v[e] : v[e] * p.in_slope;
       }
       u32x4_t h, l;
+      rg.add8(v);
       split8(v, h, l);
       bh[r] = __builtin_bit_cast(f16x8, h);
       bl[r] = __builtin_bit_cast(f16x8, l);
@@ -363,6 +366,7 @@ extern "C" int dcvc_internal_sgemm(const dcvc_conv_args *a, void *stream) {
   if ((a->res.ptr && a->res.dtype != DCVC_F32) || (a->res2.ptr && a->res2.dtype != DCVC_F32))
     return DCVC_HIP_EUNSUPPORTED;
   GP p{};
+  p.ovf = dcvc_internal_split_flag();
   p.x = reinterpret_cast<const float *>(a->x.ptr);
   p.xcs = a->x.cstride;
   p.xco = a->x.coff;

@@ -53,6 +53,7 @@ struct LP {
   const float *b1, *b2, *scale;
   int hidden;
   float slope;
+  int *ovf;               // fp16 range guard (split.h SplitRange)
 };
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void *base, int bytes) {
@@ -61,6 +62,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void *base, int byt
 
 template <int C>
 __global__ void __launch_bounds__(kNT) slffn_kernel(LP p) {
+  SplitRange rg(p.ovf);
   constexpr int KC = C / 32;        // ffn1 K chunks
   constexpr int NTW = C / 64;       // ffn2 output row blocks per wave
   constexpr int XI = KC * P * 32;   // halves of the input image (hi or lo)
@@ -107,6 +109,7 @@ __global__ void __launch_bounds__(kNT) slffn_kernel(LP p) {
       const f32x4 b = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, o + 16, 0, 0));
       const float v[8] = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
       u32x4_t h, l;
+      rg.add8(v);
       split8(v, h, l);
       const int off = swz((c8 >> 2) * P + px, c8 & 3);
       *reinterpret_cast<u32x4_t *>(Xh + off) = h;
@@ -174,6 +177,7 @@ __global__ void __launch_bounds__(kNT) slffn_kernel(LP p) {
         const float t = (hm[pb][e] + hc[pb][e] * kLoInv) + Lb1[s * HS + wave * 16 + g * 4 + e];
         v[e] = t >= 0.f ? t : t * slope;
       }
+      rg.add4(v);
       const auto h0 = __builtin_amdgcn_cvt_pkrtz(v[0], v[1]);
       const auto h1 = __builtin_amdgcn_cvt_pkrtz(v[2], v[3]);
       const uint32_t l0 = pk((v[0] - (float)h0[0]) * 2048.f, (v[1] - (float)h0[1]) * 2048.f);
@@ -258,10 +262,12 @@ struct DP {
   const uint16_t *w2;      // conv2 [C][C] as packed fragments
   int w2bytes;
   const float *b2;
+  int *ovf;               // fp16 range guard (split.h SplitRange)
 };
 
 template <int C>
 __global__ void __launch_bounds__(kNT) sldc_kernel(DP p) {
+  SplitRange rg(p.ovf);
   constexpr int KC = C / 32, NTW = C / 64, PF = 2;
   constexpr int XI = KC * P * 32;
   extern __shared__ __align__(16) unsigned char smem[];
@@ -329,6 +335,7 @@ __global__ void __launch_bounds__(kNT) sldc_kernel(DP p) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) v[e] = okp ? acc[e] + Lbd[c8 * 8 + e] : 0.f;
     u32x4_t h, l;
+    rg.add8(v);
     split8(v, h, l);
     const int off = swz((c8 >> 2) * P + px, c8 & 3);
     *reinterpret_cast<u32x4_t *>(Dh + off) = h;
@@ -461,6 +468,7 @@ extern "C" int dcvc_internal_lffn(const dcvc_ffn_args *a, void *stream) {
   if (bytes(a->x.cstride, a->x.coff) > 0x7fff0000 || bytes(a->y.cstride, a->y.coff) > 0x7fff0000)
     return DCVC_HIP_EUNSUPPORTED;
   LP p{};
+  p.ovf = dcvc_internal_split_flag();
   p.x = reinterpret_cast<const float *>(a->x.ptr);
   p.npix = (int)npix;
   p.xcs = a->x.cstride;
@@ -488,6 +496,7 @@ extern "C" int dcvc_internal_lffn(const dcvc_ffn_args *a, void *stream) {
 // 0): R / 16 x K / 32 fragments of 1024 halves (pack_frags); out NULL: size.
 extern "C" int64_t dcvc_frag_pack_weights(const float *w, int rows, int k, void *out) {
   if (!w || rows <= 0 || k <= 0 || rows % 16 || k % 32) return DCVC_HIP_EINVAL;
+  if (out && !host_split_range_ok(w, (int64_t)rows * k)) return DCVC_HIP_EINVAL;
   const int64_t n = (int64_t)rows * k * 2;
   if (out) pack_frags(w, rows, k, reinterpret_cast<uint16_t *>(out));
   return n;
@@ -507,6 +516,7 @@ extern "C" int dcvc_dw_conv2_split(const dcvc_dwc_args *a, void *stream) {
   auto bytes = [&](const dcvc_tensor &v) { return (npix * v.cstride - v.coff) * 4; };
   if (bytes(a->t) > 0x7fff0000 || bytes(a->r) > 0x7fff0000 || bytes(a->y) > 0x7fff0000) return DCVC_HIP_EUNSUPPORTED;
   DP p{};
+  p.ovf = dcvc_internal_split_flag();
   p.t = reinterpret_cast<const float *>(a->t.ptr);
   p.npix = (int)npix;
   p.H = a->t.H;

@@ -45,6 +45,29 @@ __device__ __forceinline__ void split8(const float v[8], u32x4_t &h, u32x4_t &l)
 
 constexpr float kLoInv = 1.f / 2048.f;
 
+// The fp16 range guard (dcvc_split_range_flag, include/dcvc_hip.h).  hi + 2^-11
+// lo carries a value to ~2^-21 of itself only while |v| < 2^15: above it the
+// round-toward-zero hi and then lo saturate, silently.  Every split kernel
+// keeps one of these per thread, adds each value it splits (inputs and fused
+// intermediates alike), and at exit raises *flag when the running max reached
+// 2^15.  The store is a plain vector store of one lane per wave at most.
+constexpr float kSplitMax = 32768.f;
+struct SplitRange {
+  float m = 0.f;
+  int *flag;
+  __device__ explicit SplitRange(int *f) : flag(f) {}
+  __device__ __forceinline__ void add4(const float *v) {
+    m = fmaxf(m, fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
+  }
+  __device__ __forceinline__ void add8(const float *v) {
+    add4(v);
+    add4(v + 4);
+  }
+  __device__ ~SplitRange() {
+    if (flag && m >= kSplitMax) *flag = 1;
+  }
+};
+
 __device__ __forceinline__ void wait_vm_lgkm() { __builtin_amdgcn_s_waitcnt(0x0070); }   // vmcnt(0) lgkmcnt(0)
 // vmcnt(N) lgkmcnt(0): all but the N youngest vector-memory operations done
 template <int N>
@@ -94,6 +117,13 @@ static inline float host_h2f(uint16_t h) {
     std::memcpy(&f, &u, 4);
   }
   return (h & 0x8000u) ? -f : f;
+}
+// weights enter the split through host_split: the range of SplitRange holds
+// for them too (a packer rejects a weight with |w| >= 2^15, or a NaN)
+static inline bool host_split_range_ok(const float *w, int64_t n) {
+  for (int64_t i = 0; i < n; ++i)
+    if (!(std::fabs(w[i]) < 32768.f)) return false;
+  return true;
 }
 // w = hi + 2^-11 lo: hi = f16(w), lo = f16((w - hi) * 2^11)
 static inline void host_split(float w, uint16_t &hi, uint16_t &lo) {

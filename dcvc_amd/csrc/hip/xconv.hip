@@ -61,6 +61,7 @@ struct XP {
   int64_t wchunk;          // halves of one full chunk's packed weights (hi + lo)
   const float *bias;
   const float *scale;
+  int *ovf;               // fp16 range guard (split.h SplitRange)
 };
 
 template <typename F, int... I>
@@ -108,6 +109,7 @@ __host__ __device__ constexpr int st_row(int s) { return s - st_chunk<KT, CH>(s)
 
 template <int CIN, int BN, int RW, int NW, bool R2>
 __global__ void __launch_bounds__(NW * 64) xconv3_kernel(XP p) {
+  SplitRange rg(p.ovf);
   typedef XG<CIN, BN, RW, NW, R2> G;
   constexpr int NTH = G::NTH, NT = G::NT, IH = G::IH, IW = G::IW, IWP = G::IWP, IMG = G::IMG;
   constexpr int WST = G::WST, CH = G::CH, KT = G::KT, TPKL = G::TPKL, ROWSL = G::ROWSL, NST = G::NST;
@@ -224,6 +226,7 @@ __global__ void __launch_bounds__(NW * 64) xconv3_kernel(XP p) {
 #pragma unroll
     for (int u = 0; u < PP; ++u) {
       u32x4_t h, l;
+      rg.add8(pf[u]);
       split8(pf[u], h, l);
       const int o = last ? lofs[u] : fofs[u];
       const bool ok = (u + 1) * NTH <= NTOT || (last ? lpix[u] : fpix[u]) >= 0;
@@ -606,6 +609,7 @@ extern "C" int dcvc_internal_xconv(const dcvc_conv_args *a, void *stream) {
     return DCVC_HIP_EUNSUPPORTED;
   if (a->in_op == DCVC_IN_LRELU && !(a->in_slope >= 0.f && a->in_slope <= 1.f)) return DCVC_HIP_EUNSUPPORTED;
   XP p{};
+  p.ovf = dcvc_internal_split_flag();
   p.x = reinterpret_cast<const float *>(a->x.ptr);
   p.H = a->x.H;
   p.W = a->x.W;

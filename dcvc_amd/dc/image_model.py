@@ -9,7 +9,7 @@ import torch
 
 from .. import hip as K
 from ..hip import F32, ACT_LRELU, ACT_CLAMP01
-from ..layers import Ctx, Precision, DepthConvBlock, ResidualBlockWithStride, ResidualBlockUpsample, UNet
+from ..layers import split_guarded, Ctx, Precision, DepthConvBlock, ResidualBlockWithStride, ResidualBlockUpsample, UNet
 from ..entropy import ScaleTable, FactorizedTable, EntropyCoder
 from ..stream_helper import get_downsampled_shape, encode_i, decode_i, filesize, get_state_dict
 from .common import SymbolBuffer, QuadtreePrior, BitCounter, bits_result, pad_for_y, crop_to, q_fine, curr_q
@@ -21,7 +21,7 @@ class IntraNoAR:
                  device=None):
         self.N = N
         self.ec_thread, self.stream_part = ec_thread, stream_part
-        self.prec = precision if precision is not None else Precision.fast()
+        self.prec = precision if precision is not None else Precision.split()
         self.dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
         self.entropy_coder = None
 
@@ -179,6 +179,7 @@ class IntraNoAR:
         y_hat = self.prior.decode(params, lambda idx: ec.decode(idx, self.scale_table.table), self.scale_table)
         return {"x_hat": self._decode_image(y_hat, q_dec)}
 
+    @split_guarded
     def encode_decode(self, x, q_in_ckpt, q_index, output_path=None, pic_width=None, pic_height=None):
         """image_model.py:169-196: write mode, or estimate mode when
         output_path is None."""

@@ -15,7 +15,7 @@ import torch
 
 from .. import hip as K
 from ..hip import F32, ACT_LRELU, ACT_CLAMP01
-from ..layers import (Ctx, Precision, DepthConvBlock, ResidualBlockWithStride, ResidualBlockUpsample,
+from ..layers import (split_guarded, Ctx, Precision, DepthConvBlock, ResidualBlockWithStride, ResidualBlockUpsample,
                       ResBlock, UNet, SpyNet, Grids, hyper_enc, hyper_dec, cast)
 from ..entropy import ScaleTable, FactorizedTable, EntropyCoder
 from ..stream_helper import (get_downsampled_shape, encode_p, decode_p, filesize, get_state_dict)
@@ -47,7 +47,7 @@ class DMC:
                  device=None):
         self.anchor_num = anchor_num
         self.ec_thread, self.stream_part = ec_thread, stream_part
-        self.prec = precision if precision is not None else Precision.fast()
+        self.prec = precision if precision is not None else Precision.split()
         self.dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
         self.entropy_coder = None
         self.sd = None
@@ -418,6 +418,7 @@ class DMC:
                       "ref_y": y_hat, "ref_mv_y": mv_y_hat}
         return out
 
+    @split_guarded
     def encode_decode(self, x, dpb, q_in_ckpt, q_index, output_path=None, pic_width=None, pic_height=None,
                       frame_idx=0):
         """video_model.py:522-557: write mode (output_path given: real

@@ -9,7 +9,7 @@ import torch
 
 from .. import hip as K
 from ..hip import F32, ACT_CLAMP01
-from ..layers import Ctx, Precision, hyper_enc, hyper_dec
+from ..layers import split_guarded, Ctx, Precision, hyper_enc, hyper_dec
 from ..entropy import ScaleTable, FactorizedTable
 from ..stream_helper import get_downsampled_shape, filesize, get_state_dict
 from ..dc.common import SymbolBuffer, BitCounter, bits_result
@@ -23,7 +23,7 @@ class IntraNoAR:
     def __init__(self, N=192, anchor_num=4, precision=None, device=None):
         self.N = N
         self.anchor_num = anchor_num
-        self.prec = precision if precision is not None else Precision.fast()
+        self.prec = precision if precision is not None else Precision.split()
         self.dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
         self.entropy_coder = None
 
@@ -144,6 +144,7 @@ class IntraNoAR:
         return {"x_hat": x_hat.nchw_view(), "bit": r["bit"], "bpp": r["bpp"], "bpp_y": r["bpp_y"],
                 "bpp_z": r["bpp_z"]}
 
+    @split_guarded
     def encode_decode(self, x, q_scale, output_path=None, pic_width=None, pic_height=None):
         """image_model.py:106-131."""
         if output_path is None:

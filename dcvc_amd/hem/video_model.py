@@ -15,7 +15,7 @@ import torch
 
 from .. import hip as K
 from ..hip import F32, ACT_LRELU, ACT_CLAMP01
-from ..layers import Ctx, Precision, SpyNet, Grids, ResidualBlockWithStride, hyper_enc, hyper_dec
+from ..layers import split_guarded, Ctx, Precision, SpyNet, Grids, ResidualBlockWithStride, hyper_enc, hyper_dec
 from ..entropy import ScaleTable, FactorizedTable
 from ..stream_helper import get_downsampled_shape, filesize, get_state_dict
 from ..dc.common import SymbolBuffer, BitCounter, bits_result
@@ -30,7 +30,7 @@ CH_MV, CH_N, CH_M = 64, 64, 96  # video_model.py:140-142
 class DMC:
     def __init__(self, anchor_num=4, precision=None, device=None):
         self.anchor_num = anchor_num
-        self.prec = precision if precision is not None else Precision.fast()
+        self.prec = precision if precision is not None else Precision.split()
         self.dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
         self.entropy_coder = None
 
@@ -332,6 +332,7 @@ class DMC:
         out["dpb"] = {"ref_frame": x_hat.nchw_view(), "ref_feature": feature, "ref_y": y_hat, "ref_mv_y": mv_y_hat}
         return out
 
+    @split_guarded
     def encode_decode(self, x, dpb, output_path=None, pic_width=None, pic_height=None, mv_y_q_scale=None,
                       y_q_scale=None):
         """video_model.py:377-415."""

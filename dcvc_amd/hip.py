@@ -12,7 +12,7 @@ import threading
 import numpy as np
 import torch
 
-from ._native import hip_lib, check
+from ._native import NativeError, hip_lib, check
 
 F32, BF16 = 0, 1
 F16X3 = 2   # conv compute only: split-fp16 operands, fp32 views (dcvc_hip.h DCVC_F16X3)
@@ -74,6 +74,7 @@ HIP_SYMBOLS = [
     ("dcvc_conv_pack_weights", ctypes.c_int64, [_vp, _i, _i, _i, _i, _i, _vp]),
     ("dcvc_conv2d", _i, [ctypes.POINTER(CConvArgs), _vp]),
     ("dcvc_set_option", _i, [ctypes.c_char_p, _i]),
+    ("dcvc_split_range_flag", _i, [_vp]),
     ("dcvc_last_kernel", ctypes.c_char_p, []),
     ("dcvc_depthconv_block", _i, [ctypes.POINTER(CDcbArgs), _vp]),
     ("dcvc_ffn_pack_weights", ctypes.c_int64, [_vp, _vp, _i, _i, _vp]),
@@ -171,6 +172,36 @@ _tls = threading.local()
 # Experiment switch (DCVC_BLOCKING_COPIES=1): host<->device symbol / index
 # transfers as blocking copies instead of async copies on the stream.
 ASYNC_COPIES = os.environ.get("DCVC_BLOCKING_COPIES", "0") != "1"
+
+
+class SplitRangeError(NativeError):
+    """A value entering a split-fp16 product was outside the split's range
+    (|v| >= 2^15, dcvc_split_range_flag): the frame's result would not carry the
+    ~2^-21 operand precision Precision.split() promises."""
+
+
+def split_guard_arm(device):
+    """Arm the fp16 range guard of the split kernels for the calling host
+    thread (one device int32 flag per thread and device; the kernels launched
+    from this thread raise it)."""
+    g = getattr(_tls, "split_flag", None)
+    if g is None or g.device != device:
+        g = torch.zeros(1, dtype=torch.int32, device=device)
+        _tls.split_flag = g
+        check(lib().dcvc_split_range_flag(g.data_ptr()), "split_range_flag")
+    return g
+
+
+def split_guard_check(what="frame"):
+    """Read and clear the calling thread's range flag (synchronises the current
+    stream); raise SplitRangeError when a split kernel raised it."""
+    g = getattr(_tls, "split_flag", None)
+    if g is None:
+        return
+    if int(g.item()):
+        g.zero_()
+        raise SplitRangeError(f"{what}: a value entering a split-fp16 product had |v| >= 2^15, beyond the split's "
+                              "range (hi + 2^-11 lo of fp16); code this input with Precision.parity()")
 
 
 def pinned(key, n, dtype):

@@ -58,6 +58,24 @@ class Precision:
         return "fast" if self.latent_compute == F32 else "fast-bf16-tail"
 
 
+def split_guarded(fn):
+    """encode_decode of a codec in Precision.split(): arm the fp16 range guard
+    of the split kernels (dcvc_split_range_flag) for the calling thread before
+    the frame and check it after, raising hip.SplitRangeError instead of
+    returning a frame whose split operands saturated."""
+    import functools
+
+    @functools.wraps(fn)
+    def run(self, *args, **kw):
+        if self.prec.feat_compute != F16X3:
+            return fn(self, *args, **kw)
+        K.split_guard_arm(self.dev)
+        out = fn(self, *args, **kw)
+        K.split_guard_check(f"{type(self).__name__}.encode_decode")
+        return out
+    return run
+
+
 class Ctx:
     """Builds layers from a state_dict on one device under one precision."""
 

@@ -105,6 +105,16 @@ int dcvc_conv2d(const dcvc_conv_args *a, void *stream);
  * "conv3x3_resident" = 1 (default) prefers its persistent resident-weight
  * variant where the weights fit in LDS. */
 int dcvc_set_option(const char *name, int value);
+/* fp16 range guard of the split-fp16 kernels (compute DCVC_F16X3 and the fused
+ * split blocks): a split operand carries an fp32 value v as hi + 2^-11 lo of two
+ * fp16 numbers, to ~2^-21 of v while |v| < 2^15, and saturates silently above.
+ * With `flag` (a device int32) set, every split kernel launched afterwards from
+ * the calling host thread sets *flag = 1 when any value it splits (an input or
+ * a fused intermediate) has |v| >= 2^15; the caller reads and clears it once per
+ * frame and raises instead of returning an out-of-range result.  NULL (the
+ * default) turns the guard off for the thread.  No reference counterpart: the
+ * reference computes in fp32 (DCVC-DC/src/models/video_net.py, layers.py). */
+int dcvc_split_range_flag(int *flag);
 /* Kernel instantiation launched by the last dcvc_conv2d / dcvc_depthconv_block
  * call on the calling host thread, spelled as rocprofv3 reports it, with the
  * grid size in work-items (e.g. "conv3x3_kernel<48, 16, false, unsigned

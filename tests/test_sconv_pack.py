@@ -63,10 +63,23 @@ def test_pack_f16x3_roundtrip(cout, cin, k):
 
 
 def test_pack_f16x3_hi_is_round_to_nearest():
-    w = torch.tensor([1.0 + 2 ** -11, 1.0 + 3 * 2 ** -11, -0.1, 65000.0]).view(4, 1, 1, 1)
+    w = torch.tensor([1.0 + 2 ** -11, 1.0 + 3 * 2 ** -11, -0.1, 32760.0]).view(4, 1, 1, 1)
     buf = pack(w)
     hi = buf[:4 * 32].view(np.float16).reshape(4, 32)[:, 0].astype(np.float64)
-    assert hi.tolist() == [1.0, 1.0 + 4 * 2 ** -11, float(np.float16(-0.1)), 64992.0]
+    assert hi.tolist() == [1.0, 1.0 + 4 * 2 ** -11, float(np.float16(-0.1)), 32768.0]
+
+
+@pytest.mark.parametrize("bad", [32768.0, -65000.0, float("inf"), float("nan")])
+def test_pack_f16x3_rejects_out_of_range(bad):
+    """A weight outside the split's range (|w| >= 2^15: the fp16 hi / lo pair no
+    longer carries it to ~2^-21) is rejected, as the kernels' range guard
+    rejects such activations (tests/test_gpu_split_range.py)."""
+    from dcvc_amd import hip as h
+    wn = np.array([0.5, bad, 1.0, 2.0], np.float32).reshape(4, 1, 1, 1)
+    n = h.lib().dcvc_conv_pack_weights(wn.ctypes.data_as(ctypes.c_void_p), 4, 1, 1, 1, h.F16X3, None)
+    out = np.zeros(n, dtype=np.uint16)
+    assert h.lib().dcvc_conv_pack_weights(wn.ctypes.data_as(ctypes.c_void_p), 4, 1, 1, 1, h.F16X3,
+                                          out.ctypes.data_as(ctypes.c_void_p)) == -1
 
 
 @pytest.mark.parametrize("c,hid", [(48, 192), (128, 512), (32, 128)])
