@@ -588,7 +588,6 @@ extern "C" void dcvc_internal_sgemm_pd(int v);
 extern "C" int dcvc_internal_set_option_split(const char *name, int value);
 extern "C" int dcvc_internal_xconv(const dcvc_conv_args *a, void *stream);
 extern "C" void dcvc_internal_xconv_enable(int v);
-extern "C" void dcvc_internal_xconv_waves(int v);
 
 // fp16 range guard of the split kernels (split.h SplitRange): one flag per
 // calling host thread (concurrent GOP lanes each launch from their own thread
@@ -807,10 +806,6 @@ extern "C" int dcvc_set_option(const char *name, int value) {
   }
   if (std::strcmp(name, "xconv") == 0) {
     dcvc_internal_xconv_enable(value);
-    return DCVC_HIP_OK;
-  }
-  if (std::strcmp(name, "xconv_waves") == 0) {
-    dcvc_internal_xconv_waves(value);
     return DCVC_HIP_OK;
   }
   if (std::strcmp(name, "conv3x3_rows4") == 0) {

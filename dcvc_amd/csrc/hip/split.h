@@ -45,6 +45,29 @@ __device__ __forceinline__ void split8(const float v[8], u32x4_t &h, u32x4_t &l)
 
 constexpr float kLoInv = 1.f / 2048.f;
 
+// Compiler fences on a value (device pass only: the host pass sees kernel
+// bodies too, and x86 has no "s" register class): after opaque_v(x) /
+// opaque_s(x) the compiler must assume x changed, so it neither hoists nor
+// shares (CSE) computations on x across the fence.  Free in the ISA.
+template <typename T>
+__device__ __forceinline__ void opaque_v(T &x) {
+#ifdef __HIP_DEVICE_COMPILE__
+  asm volatile("" : "+v"(x));
+#endif
+}
+// no instruction is scheduled across this point (device pass only)
+__device__ __forceinline__ void sched_fence() {
+#ifdef __HIP_DEVICE_COMPILE__
+  __builtin_amdgcn_sched_barrier(0);
+#endif
+}
+template <typename T>
+__device__ __forceinline__ void opaque_s(T &x) {
+#ifdef __HIP_DEVICE_COMPILE__
+  asm volatile("" : "+s"(x));
+#endif
+}
+
 // The fp16 range guard (dcvc_split_range_flag, include/dcvc_hip.h).  hi + 2^-11
 // lo carries a value to ~2^-21 of itself only while |v| < 2^15: above it the
 // round-toward-zero hi and then lo saturate, silently.  Every split kernel
@@ -58,6 +81,9 @@ struct SplitRange {
   __device__ explicit SplitRange(int *f) : flag(f) {}
   __device__ __forceinline__ void add4(const float *v) {
     m = fmaxf(m, fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
+    // fold now: left to itself the compiler keeps every partial max live
+    // until the kernel's end (tens of registers in a long unrolled kernel)
+    opaque_v(m);
   }
   __device__ __forceinline__ void add8(const float *v) {
     add4(v);

@@ -14,8 +14,8 @@
 //
 //   stage = one K step of 32 (one tap of a 32-channel chunk, or 2 / 4 packed
 //           taps of a 16- / 8-channel last chunk), one workgroup barrier;
-//   weights: streamed through a ring of three LDS slots by LDS-DMA, issued
-//           two stages ahead (L2-resident: every tile reads the same weights);
+//   weights: streamed through a ring of four LDS slots by LDS-DMA, issued
+//           three stages ahead (L2-resident: every tile reads the same weights);
 //   operands: the next stage's A (weights) and B (image) fragments are read
 //           from LDS while the current stage's MFMAs run (two register sets),
 //           so no wave waits on LDS latency at a stage start;
@@ -73,7 +73,7 @@ __device__ __forceinline__ void sfor(F &&f) {
   sfor_(f, std::make_integer_sequence<int, N>{});
 }
 
-template <int CIN, int BN, int RW, int NW, bool R2>
+template <int CIN, int BN, int RW, int NW, int NRES>
 struct XG {
   static constexpr int KT = 9, NTH = NW * 64, TH = NW * RW, NT = BN / 16;
   static constexpr int IH = TH + 2, IW = 18, IWP = 20;
@@ -90,15 +90,34 @@ struct XG {
   static constexpr int WST = BN * 32;                       // halves per weight stage (hi or lo)
   static constexpr int NDMA = 2 * BN / 16;                  // 1-KiB LDS-DMA pieces per stage
   static constexpr int DPW = (NDMA + NW - 1) / NW;          // ... per wave (every wave issues DPW)
-  // LDS (halves): [2 image buffers][hi, lo][IMG] | [3 weight slots][hi, lo][WST] | DMA sink 512 | consts
+  // weight ring: NSW slots, the DMA of a stage issued AH = NSW - 1 stages ahead
+  static constexpr int NSW = 4, AH = NSW - 1;
+  // LDS (halves): [2 image buffers][hi, lo][IMG] | [NSW weight slots][hi, lo][WST] | DMA sink 512 | consts
   static constexpr int L_W = 4 * IMG;
-  static constexpr int L_SINK = L_W + 6 * WST;
+  static constexpr int L_SINK = L_W + 2 * NSW * WST;
   static constexpr int L_C = L_SINK + 512;
   static constexpr size_t lds(int cout) { return (size_t)L_C * 2 + (size_t)2 * cout * 4; }
   // vector-memory instructions per thread: image chunk loads, tile loads (res, res2), epilogue stores
   static constexpr int NIMG = 2 * PPM;
-  static constexpr int NTILE = (R2 ? 2 : 1) * RW * NT;
+  static constexpr int NTILE = NRES * RW * NT;
   static constexpr int NSTORE = RW * NT;
+  // vector-memory instructions per thread issued by stage x of a tile after
+  // its weight DMA, and in all
+  static constexpr int after_dma(int x) {
+    return (st_row_(x) == 0 ? NIMG : 0) + (x == 0 ? NTILE : 0) + (x == NST - 1 ? NSTORE : 0);
+  }
+  static constexpr int all_ops(int x) { return DPW + after_dma(x); }
+  static constexpr int st_row_(int x) { return x < (CH - 1) * KT ? x % KT : x - (CH - 1) * KT; }
+  // stage s + 1 reads the weight fragments of stage s + 2 (after its MFMAs),
+  // so at the end of stage s the weights of stage s + 2 must have landed:
+  // their DMA was issued by stage s + 2 - AH (of this tile or the previous
+  // one, the schedule repeats per tile); the operations issued after it may
+  // stay in flight (vmcnt counts them in issue order)
+  static constexpr int wait_n(int s) {
+    int n = after_dma((s + 2 - AH + 2 * NST) % NST);
+    for (int k = 1; k < AH - 1; ++k) n += all_ops((s + 2 - AH + k + 2 * NST) % NST);
+    return n;
+  }
 };
 
 // stage s of a tile -> (chunk, row of the chunk)
@@ -107,10 +126,10 @@ __host__ __device__ constexpr int st_chunk(int s) { return s < (CH - 1) * KT ? s
 template <int KT, int CH>
 __host__ __device__ constexpr int st_row(int s) { return s - st_chunk<KT, CH>(s) * KT; }
 
-template <int CIN, int BN, int RW, int NW, bool R2>
+template <int CIN, int BN, int RW, int NW, int NRES>
 __global__ void __launch_bounds__(NW * 64) xconv3_kernel(XP p) {
+  typedef XG<CIN, BN, RW, NW, NRES> G;
   SplitRange rg(p.ovf);
-  typedef XG<CIN, BN, RW, NW, R2> G;
   constexpr int NTH = G::NTH, NT = G::NT, IH = G::IH, IW = G::IW, IWP = G::IWP, IMG = G::IMG;
   constexpr int WST = G::WST, CH = G::CH, KT = G::KT, TPKL = G::TPKL, ROWSL = G::ROWSL, NST = G::NST;
   constexpr int NDMA = G::NDMA, DPW = G::DPW, PPF = G::PPF, PPL = G::PPL, PPM = G::PPM;
@@ -120,7 +139,7 @@ __global__ void __launch_bounds__(NW * 64) xconv3_kernel(XP p) {
   float *const Lc = reinterpret_cast<float *>(smem + (size_t)G::L_C * 2);
 
   const int tid = threadIdx.x;
-  const int wave = tid >> 6, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;   // wave-uniform
   const int col = lane & 15, hi = lane >> 4;
   const int GR = gridDim.x;
   int g = blockIdx.x;
@@ -133,29 +152,24 @@ __global__ void __launch_bounds__(NW * 64) xconv3_kernel(XP p) {
     Lc[p.cout + i] = p.scale ? p.scale[i] : 1.f;
   }
 
-  // ---- image piece plans (per thread, constant).  Piece u of a chunk with
-  // NS staged 8-channel slots = (halo row iy, halo column ix, slot): its
-  // element offset from the tile's first halo pixel (prel), its LDS half
-  // offset (lofs), its halo position (ipix: iy << 8 | ix, -1 past the plan)
+  // ---- image piece plan.  Piece u of a chunk with NS staged 8-channel slots
+  // = (halo row iy, halo column ix, slot), recomputed where it is used (a few
+  // VALU with constant divisors) rather than kept live through the kernel
   constexpr int NTOTF = IH * IW * 4, NTOTL = IH * IW * G::NSLL;
-  int fprel[PPF], fofs[PPF], fpix[PPF], lprel[PPL], lofs[PPL], lpix[PPL];
-#pragma unroll
-  for (int u = 0; u < PPF; ++u) {
+  struct Piece {
+    int iy, ix, slot, valid;
+  };
+  auto piece = [&](int u, auto NS_) {
+    constexpr int NS = decltype(NS_)::value;
     const int it = tid + u * NTH;
-    const int slot = it & 3, pix = it >> 2, iy = pix / IW, ix = pix - iy * IW;
-    fpix[u] = it < NTOTF ? (iy << 8) | ix : -1;
-    fofs[u] = swzx(iy * IWP + ix, ix, slot);
-    fprel[u] = (iy * p.W + ix) * p.xcs + slot * 8;
-  }
-#pragma unroll
-  for (int u = 0; u < PPL; ++u) {
-    constexpr int NS = G::NSLL;
-    const int it = tid + u * NTH;
-    const int slot = it % NS, pix = it / NS, iy = pix / IW, ix = pix - iy * IW;
-    lpix[u] = it < NTOTL ? (iy << 8) | ix : -1;
-    lofs[u] = swzx(iy * IWP + ix, ix, slot);
-    lprel[u] = (iy * p.W + ix) * p.xcs + slot * 8;
-  }
+    const int pix = it / NS;
+    Piece q;
+    q.slot = it - pix * NS;
+    q.iy = pix / IW;
+    q.ix = pix - q.iy * IW;
+    q.valid = it < IH * IW * NS;
+    return q;
+  };
   float pf[PPM][8];   // image pieces in flight (one chunk)
 
   struct TI {
@@ -192,14 +206,13 @@ __global__ void __launch_bounds__(NW * 64) xconv3_kernel(XP p) {
     for (int u = 0; u < PPM; ++u) {
       int o = 0x7fffffe0;
       if (u < PP) {
-        const int pq = last ? lpix[u < PPL ? u : 0] : fpix[u < PPF ? u : 0];
-        const int pr = last ? lprel[u < PPL ? u : 0] : fprel[u < PPF ? u : 0];
-        o = (toff + pr) * 4;
+        const Piece q = piece(u, std::integral_constant<int, last ? G::NSLL : 4>{});
+        o = (toff + (q.iy * p.W + q.ix) * p.xcs + q.slot * 8) * 4;
         if (!inner) {
-          const int gy = iy0 + (pq >> 8), gx = ix0 + (pq & 255);
+          const int gy = iy0 + q.iy, gx = ix0 + q.ix;
           if (!((unsigned)gy < (unsigned)p.H && (unsigned)gx < (unsigned)p.W)) o = 0x7fffffe0;
         }
-        if ((u + 1) * NTH > NTOT && pq < 0) o = 0x7fffffe0;
+        if ((u + 1) * NTH > NTOT && !q.valid) o = 0x7fffffe0;
       }
       const f32x4 a = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, o, 0, 0));
       const f32x4 b = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, o + 16, 0, 0));
@@ -228,8 +241,9 @@ __global__ void __launch_bounds__(NW * 64) xconv3_kernel(XP p) {
       u32x4_t h, l;
       rg.add8(pf[u]);
       split8(pf[u], h, l);
-      const int o = last ? lofs[u] : fofs[u];
-      const bool ok = (u + 1) * NTH <= NTOT || (last ? lpix[u] : fpix[u]) >= 0;
+      const Piece q = piece(u, std::integral_constant<int, last ? G::NSLL : 4>{});
+      const int o = swzx(q.iy * IWP + q.ix, q.ix, q.slot);
+      const bool ok = (u + 1) * NTH <= NTOT || q.valid;
       if (ok) {
         *reinterpret_cast<u32x4_t *>(Lh + o) = h;
         *reinterpret_cast<u32x4_t *>(Lh + IMG + o) = l;
@@ -237,11 +251,13 @@ __global__ void __launch_bounds__(NW * 64) xconv3_kernel(XP p) {
     }
   };
 
-  // LDS-DMA of the weights of stage s (n-block n0) into slot ws: 16 rows of
-  // 64 bytes per instruction; lane i writes physical slot i % 4 of row i / 4,
-  // so it reads the logical slot the swizzle puts there (rows past cout:
-  // zeros).  Every wave issues DPW instructions (the surplus into a sink).
-  // The lane's part of the source offset is fixed: dlane[d]
+  // LDS-DMA of the weights of stage s into slot ws: 16 rows of 64 bytes per
+  // instruction; lane i writes physical slot i % 4 of row i / 4, so it reads
+  // the logical slot the swizzle puts there.  Every wave issues DPW
+  // instructions (the surplus into a sink).  The source offset is split into a
+  // per-lane part (dv: the lane's row and slot, or out of range for rows past
+  // cout and sink pieces; fixed per tile) and a uniform part (soffset: chunk,
+  // hi / lo block, kernel row, n-block)
   const __amdgpu_buffer_rsrc_t wr =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t *>(p.w), (short)0, p.wbytes, 0x00020000);
   int dlane[DPW], drow[DPW];
@@ -252,28 +268,35 @@ __global__ void __launch_bounds__(NW * 64) xconv3_kernel(XP p) {
     const int R = k * 16 + (lane >> 2);
     const int ls = (lane & 3) ^ ((0x1320 >> (((R >> 2) & 3) << 2)) & 3);
     dlane[d] = (R * 32 + ls * 8) * 2;
-    drow[d] = R;
+    drow[d] = i < NDMA ? R : 0x7fff;
   }
-  auto dma_w = [&](int n0, auto s_, int ws) {
+  // per-lane DMA offsets of an n-block starting at n0
+  auto dma_lanes = [&](int n0, int (&dv)[DPW]) {
+#pragma unroll
+    for (int d = 0; d < DPW; ++d) dv[d] = drow[d] < p.cout - n0 ? dlane[d] : 0x7ffffff0;
+  };
+  int wcb = (int)(p.wchunk * 2), wrb = p.cout * 64;   // bytes per full chunk, per kernel row (hi or lo block)
+  auto dma_w = [&](int n0, const int (&dv)[DPW], auto s_, int ws) {
     constexpr int s = decltype(s_)::value;
     constexpr int c = st_chunk<KT, CH>(s), rr = st_row<KT, CH>(s);
     constexpr int rows = c == CH - 1 ? ROWSL : KT;
-    const int nleft = p.cout - n0;
 #pragma unroll
     for (int d = 0; d < DPW; ++d) {
       const int i = wave + NW * d;   // wave-uniform
       const int hl = i >= NDMA / 2, k = hl ? i - NDMA / 2 : i;
-      const int ub = (int)(((int64_t)c * p.wchunk + (hl ? (int64_t)rows * p.cout * 32 : 0) +
-                            ((int64_t)rr * p.cout + n0) * 32) * 2);
-      int voff = ub + dlane[d];
-      if (!(i < NDMA && drow[d] < nleft)) voff = 0x7ffffff0;
+      const int ub = c * wcb + (hl ? rows * wrb : 0) + rr * wrb + n0 * 64;
       uint16_t *dst = i < NDMA ? L + G::L_W + ws * 2 * WST + hl * WST + k * 512 : L + G::L_SINK;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(wr, (__attribute__((address_space(3))) void *)dst, 16, voff, 0, 0, 0);
+      // device pass only: with a non-constant soffset the host pass drops the
+      // kernel's launch stubs without a diagnostic
+#ifdef __HIP_DEVICE_COMPILE__
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(wr, (__attribute__((address_space(3))) void *)dst, 16, dv[d], ub, 0,
+                                               0);
+#endif
     }
   };
 
   // per-lane operand offsets (halves): weights (row j * 16 + col, slot hi)
-  const int aoff = swz(col, hi);
+  int aoff = swz(col, hi);
   // image, one tap per K step: pixel (wave rows + dy, col + dx), slot hi
   int bo1[3], bo2[3];
 #pragma unroll
@@ -286,19 +309,22 @@ __global__ void __launch_bounds__(NW * 64) xconv3_kernel(XP p) {
   }
   const int sub = hi / (4 / TPKL);
 
-  f16x8 oa[2][NT][2], ob[2][RW][2];   // [set][frag][hi, lo]
-  // LDS -> registers: the fragments of stage s (image buffer ib, weight slot ws) into set S
-  auto read_ops = [&](auto S_, auto s_, int ib, int ws) {
+  // operand registers: one set of weight fragments (each refilled with the
+  // next stage's fragment right after its last MFMA of this stage) and two
+  // sets of image fragments (the next stage's read at the stage start)
+  f16x8 oa[NT][2], ob[2][RW][2];   // [frag][hi, lo], [set][frag][hi, lo]
+  // LDS -> registers: weight fragment j of stage s (weight slot ws)
+  auto read_a = [&](int j, int ws) {
+    const uint16_t *Lw = L + G::L_W + ws * 2 * WST + aoff + j * 512;
+    oa[j][0] = *reinterpret_cast<const f16x8 *>(Lw);
+    oa[j][1] = *reinterpret_cast<const f16x8 *>(Lw + WST);
+  };
+  // LDS -> registers: the image fragments of stage s (image buffer ib) into set S
+  auto read_b = [&](auto S_, auto s_, int ib) {
     constexpr int S = decltype(S_)::value;
     constexpr int s = decltype(s_)::value;
     constexpr int c = st_chunk<KT, CH>(s), rr = st_row<KT, CH>(s);
     constexpr int tpk = c == CH - 1 ? TPKL : 1;
-    const uint16_t *Lw = L + G::L_W + ws * 2 * WST + aoff;
-#pragma unroll
-    for (int j = 0; j < NT; ++j) {
-      oa[S][j][0] = *reinterpret_cast<const f16x8 *>(Lw + j * 512);
-      oa[S][j][1] = *reinterpret_cast<const f16x8 *>(Lw + WST + j * 512);
-    }
     const uint16_t *Li = L + ib * 2 * IMG;
     if constexpr (tpk == 1) {
       constexpr int dy = rr / 3, dx = rr % 3;
@@ -327,16 +353,21 @@ __global__ void __launch_bounds__(NW * 64) xconv3_kernel(XP p) {
   };
 
   f32x4 am[RW][NT], ac[RW][NT];
-  auto mfmas = [&](auto S_) {
+  // the MFMAs of a stage (image set S), weight fragment by weight fragment;
+  // after fragment j's last MFMA its registers take the next stage's fragment
+  // j from weight slot wsn
+  auto mfmas = [&](auto S_, int wsn) {
     constexpr int S = decltype(S_)::value;
 #pragma unroll
-    for (int r = 0; r < RW; ++r)
+    for (int j = 0; j < NT; ++j) {
 #pragma unroll
-      for (int j = 0; j < NT; ++j) {
-        am[r][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(oa[S][j][0], ob[S][r][0], am[r][j], 0, 0, 0);
-        ac[r][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(oa[S][j][0], ob[S][r][1], ac[r][j], 0, 0, 0);
-        ac[r][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(oa[S][j][1], ob[S][r][0], ac[r][j], 0, 0, 0);
+      for (int r = 0; r < RW; ++r) {
+        am[r][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(oa[j][0], ob[S][r][0], am[r][j], 0, 0, 0);
+        ac[r][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(oa[j][0], ob[S][r][1], ac[r][j], 0, 0, 0);
+        ac[r][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(oa[j][1], ob[S][r][0], ac[r][j], 0, 0, 0);
       }
+      read_a(j, wsn);
+    }
   };
 
   // the lane's output pieces: pixel (row wave * RW + r, column col), channels
@@ -348,16 +379,16 @@ __global__ void __launch_bounds__(NW * 64) xconv3_kernel(XP p) {
   auto full_tile = [&](const TI &ti) {
     return ti.oy0 + G::TH <= p.Ho && ti.ox0 + 16 <= p.Wo && ti.n0 + BN <= p.cout;
   };
-  // tile-level register loads: residual and second residual of the lane's
-  // output pieces (always issued; zeros when absent or outside the output)
-  f32x4 rv1[RW][NT], rv2[R2 ? RW : 1][NT];
+  // tile-level register loads: the NRES residuals of the lane's output
+  // pieces (always issued; zeros outside the output)
+  f32x4 rv1[NRES >= 1 ? RW : 1][NT], rv2[NRES >= 2 ? RW : 1][NT];
   auto load_res = [&](const TI &ti) {
+    if constexpr (NRES == 0) return;
     const int64_t rowb = (int64_t)ti.oy0 * p.Wo;
-    const int nr1 = p.has_res ? 0x7fff0000 : 0;
     const __amdgpu_buffer_rsrc_t r1 = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<float *>(p.has_res ? p.res + rowb * p.rcs + p.rco : p.x), (short)0, nr1, 0x00020000);
+        const_cast<float *>(p.res + rowb * p.rcs + p.rco), (short)0, 0x7fff0000, 0x00020000);
     __amdgpu_buffer_rsrc_t r2 = r1;
-    if constexpr (R2)
+    if constexpr (NRES >= 2)
       r2 = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(p.res2 + rowb * p.r2cs + p.r2co), (short)0,
                                              0x7fff0000, 0x00020000);
     const bool full = full_tile(ti);
@@ -368,8 +399,9 @@ __global__ void __launch_bounds__(NW * 64) xconv3_kernel(XP p) {
       for (int j = 0; j < NT; ++j) {
         const bool ok = full || piece_ok(ti, r, j);
         const int o1 = ok ? ((px + r * p.Wo) * p.rcs + n + j * 16) * 4 : 0x7ffffff0;
-        rv1[r][j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r1, o1, 0, 0));
-        if constexpr (R2) {
+        if constexpr (NRES >= 1)
+          rv1[r][j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r1, o1, 0, 0));
+        if constexpr (NRES >= 2) {
           const int o2 = ok ? ((px + r * p.Wo) * p.r2cs + n + j * 16) * 4 : 0x7ffffff0;
           rv2[r][j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r2, o2, 0, 0));
         }
@@ -402,7 +434,7 @@ __global__ void __launch_bounds__(NW * 64) xconv3_kernel(XP p) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) v[r][j][e] = fmaxf(v[r][j][e], v[r][j][e] * p.slope);
     }
-    if (p.has_res) {
+    if constexpr (NRES >= 1) {
 #pragma unroll
       for (int r = 0; r < RW; ++r)
 #pragma unroll
@@ -410,7 +442,7 @@ __global__ void __launch_bounds__(NW * 64) xconv3_kernel(XP p) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) v[r][j][e] = rv1[r][j][e] + v[r][j][e];
     }
-    if constexpr (R2) {
+    if constexpr (NRES >= 2) {
 #pragma unroll
       for (int r = 0; r < RW; ++r)
 #pragma unroll
@@ -441,25 +473,43 @@ __global__ void __launch_bounds__(NW * 64) xconv3_kernel(XP p) {
       }
   };
 
-  // ---- prologue: weights of stages 0 and 1, the first chunk's image
+  // ---- prologue: weights of stages 0 .. AH - 1, the first chunk's image
   const int G0 = GR;
   {
     const TI t0 = tile_of(g);
-    dma_w(t0.n0, std::integral_constant<int, 0>{}, 0);
-    dma_w(t0.n0, std::integral_constant<int, 1>{}, 1);
+    int dv0[DPW];
+    dma_lanes(t0.n0, dv0);
+    sfor<G::AH>([&](auto k_) {
+      constexpr int k = decltype(k_)::value;
+      dma_w(t0.n0, dv0, std::integral_constant<int, k>{}, k);
+    });
     load_img(t0, std::integral_constant<int, 0>{});
   }
-  publish(0, std::integral_constant<int, 0>{});   // (waits for its own loads)
-  // stage 0's weights: the younger DMA (stage 1) may stay in flight
-  wait_vm_n_lgkm<DPW>();
+  publish(0, std::integral_constant<int, 0>{});   // (waits for its own loads, so for every DMA before them)
+  wait_vm_lgkm();
   __syncthreads();
-  read_ops(std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{}, 0, 0);
+#pragma unroll
+  for (int j = 0; j < NT; ++j) read_a(j, 0);
+  read_b(std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{}, 0);
 
-  int kw = 0;   // weight slot of the current stage (stage counter mod 3)
+  int kw = 0;   // weight slot of the current stage (stage counter mod NSW)
   int q = 0;    // image buffer of the current chunk (chunk counter mod 2)
   for (int t = g; t < p.ntiles; t += G0) {
     const int tn = t + G0 < p.ntiles ? t + G0 : t;   // the next tile (prefetch target; itself when last)
     const TI tc = tile_of(t), tx = tile_of(tn);
+    // the per-lane LDS / DMA offsets are opaque to the compiler here, so it
+    // computes each stage's addresses inside the stage (an add or two) instead
+    // of hoisting dozens of them out of the tile loop into live registers
+    opaque_v(aoff);
+#pragma unroll
+    for (int dx = 0; dx < 3; ++dx) opaque_v(bo1[dx]), opaque_v(bo2[dx]);
+#pragma unroll
+    for (int d = 0; d < DPW; ++d) opaque_v(dlane[d]), opaque_v(drow[d]);
+    opaque_s(wcb);
+    opaque_s(wrb);
+    int dvc[DPW], dvx[DPW];
+    dma_lanes(tc.n0, dvc);
+    dma_lanes(tx.n0, dvx);
 #pragma unroll
     for (int r = 0; r < RW; ++r)
 #pragma unroll
@@ -477,10 +527,18 @@ __global__ void __launch_bounds__(NW * 64) xconv3_kernel(XP p) {
       constexpr int rows = c == CH - 1 ? ROWSL : KT;
       // stage s: its weights (slot kw) and image (buffer q) are visible, its
       // operands are in register set S (read during the previous stage)
-      const int ws2 = kw + 2 >= 3 ? kw - 1 : kw + 2;
-      // 1. weights of stage s + 2 (this tile or the next) into slot kw + 2
-      if constexpr (s + 2 < NST) dma_w(tc.n0, std::integral_constant<int, (s + 2) % NST>{}, ws2);
-      else dma_w(tx.n0, std::integral_constant<int, (s + 2) % NST>{}, ws2);
+      constexpr int AH = G::AH, NSW = G::NSW;
+      // per-stage opacity of the lane offsets: an address of this stage is
+      // computed in it, never shared (CSE) with an equal one of a later stage
+      // of the tile (the same tap of another chunk in the same image buffer,
+      // the same ring slot), which would keep it live in between
+      opaque_v(aoff);
+#pragma unroll
+      for (int dx = 0; dx < 3; ++dx) opaque_v(bo1[dx]), opaque_v(bo2[dx]);
+      const int wsa = kw + AH >= NSW ? kw + AH - NSW : kw + AH;
+      // 1. weights of stage s + AH (this tile or the next) into slot kw + AH
+      if constexpr (s + AH < NST) dma_w(tc.n0, dvc, std::integral_constant<int, (s + AH) % NST>{}, wsa);
+      else dma_w(tx.n0, dvx, std::integral_constant<int, (s + AH) % NST>{}, wsa);
       // 2. the next chunk's image pieces (first stage of a chunk)
       if constexpr (rr == 0) {
         if constexpr (c + 1 < CH) load_img(tc, std::integral_constant<int, (c + 1 < CH ? c + 1 : 0)>{});
@@ -490,16 +548,14 @@ __global__ void __launch_bounds__(NW * 64) xconv3_kernel(XP p) {
       if constexpr (s == 0) load_res(tc);
       // 4. operands of stage s + 1 into the other register set (the next
       // stage's weights landed and were published one barrier ago)
-      const int ws1 = kw + 1 >= 3 ? kw - 2 : kw + 1;
+      const int ws1 = kw + 1 >= NSW ? 0 : kw + 1;
       constexpr int s1 = s + 1 < NST ? s + 1 : 0;
       constexpr int c1 = st_chunk<KT, CH>(s1);
       const int ib1 = (s + 1 < NST ? (c1 == c ? q : q ^ 1) : q ^ 1);
-      if constexpr (!late)
-        read_ops(std::integral_constant<int, S ^ 1>{}, std::integral_constant<int, s1>{}, ib1, ws1);
-      // 5. MFMAs of stage s
-      mfmas(std::integral_constant<int, S>{});
-      if constexpr (late)
-        read_ops(std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{}, ib1, ws1);
+      if constexpr (!late) read_b(std::integral_constant<int, S ^ 1>{}, std::integral_constant<int, s1>{}, ib1);
+      // 5. MFMAs of stage s (each weight fragment refilled with stage s + 1's)
+      mfmas(std::integral_constant<int, S>{}, ws1);
+      if constexpr (late) read_b(std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{}, ib1);
       // 6. the next chunk's image into the other buffer (second-to-last stage
       // of a chunk: visible at the last stage, whose operand reads need it)
       if constexpr (rr == rows - 2) {
@@ -508,22 +564,21 @@ __global__ void __launch_bounds__(NW * 64) xconv3_kernel(XP p) {
       }
       // 7. epilogue
       if constexpr (s == NST - 1) epilogue(tc);
-      // end of stage: stage s + 1's weights (the DMA issued one stage before
-      // this one) must have landed; every vector-memory operation issued
-      // after it may stay in flight: the previous stage's after its DMA, and
-      // all of this stage's
+      // end of stage: stage s + 2's weights must have landed, every
+      // vector-memory operation issued after their DMA may stay in flight
       {
-        constexpr int sp = s == 0 ? NST - 1 : s - 1;
-        constexpr int pv = (st_row<KT, CH>(sp) == 0 ? G::NIMG : 0) + (sp == 0 ? G::NTILE : 0) +
-                           (sp == NST - 1 ? G::NSTORE : 0);
-        constexpr int here = DPW + (rr == 0 ? G::NIMG : 0) + (s == 0 ? G::NTILE : 0) + (s == NST - 1 ? G::NSTORE : 0);
-        constexpr int N = pv + here;
+        constexpr int N = G::wait_n(s);
         static_assert(N < 64, "too many vector-memory operations in flight for vmcnt");
         wait_vm_n_lgkm<N>();
       }
+      // nothing of one stage is scheduled into another: the MFMAs of a stage
+      // stay between its operand reads and its barrier, so operand and
+      // accumulator registers live one stage long
+      sched_fence();
       raw_barrier();
+      sched_fence();
       if constexpr (rr == rows - 1) q ^= 1;
-      kw = kw + 1 >= 3 ? 0 : kw + 1;
+      kw = kw + 1 >= NSW ? 0 : kw + 1;
     });
   }
   wait_vm_lgkm();   // no LDS-DMA left in flight when the workgroup exits
@@ -531,11 +586,10 @@ __global__ void __launch_bounds__(NW * 64) xconv3_kernel(XP p) {
 
 int g_cus = 0;
 int g_enable = 1;   // dcvc_set_option("xconv", 0): route every split conv to sconv.hip
-int g_nw = 8;       // dcvc_set_option("xconv_waves", 4 | 8)
 
-template <int CIN, int BN, int RW, int NW, bool R2>
+template <int CIN, int BN, int RW, int NW, int NRES>
 int launch(XP p, hipStream_t st) {
-  typedef XG<CIN, BN, RW, NW, R2> G;
+  typedef XG<CIN, BN, RW, NW, NRES> G;
   const size_t lds = G::lds(p.cout);
   if (lds > 160 * 1024) return DCVC_HIP_EUNSUPPORTED;
   p.tiles_x = (p.Wo + 15) / 16;
@@ -554,30 +608,33 @@ int launch(XP p, hipStream_t st) {
   }
   int64_t grid = g_cus;
   if (grid > nt) grid = nt;
-  auto kern = xconv3_kernel<CIN, BN, RW, NW, R2>;
-  dcvc_note_kernel("xconv3_kernel<%d, %d, %d, %d, %s>@%lld", CIN, BN, RW, NW, bname(R2), (long long)grid * NW * 64);
+  auto kern = xconv3_kernel<CIN, BN, RW, NW, NRES>;
+  dcvc_note_kernel("xconv3_kernel<%d, %d, %d, %d, %d>@%lld", CIN, BN, RW, NW, NRES, (long long)grid * NW * 64);
   dcvc_ensure_lds(reinterpret_cast<const void *>(kern), 160 * 1024);
   hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(NW * 64), lds, st, p);
   DCVC_LAUNCH_CHECK();
   return DCVC_HIP_OK;
 }
 
-template <int CIN, int BN, bool R2>
-int pick_nw(XP p, hipStream_t st) {
-  if (g_nw == 4) return launch<CIN, BN, 4, 4, R2>(p, st);
-  return launch<CIN, BN, 2, 8, R2>(p, st);
-}
+// the residual count picks the instantiation; 8 waves of 2 output rows each
 template <int CIN, int BN>
-int pick_r2(XP p, hipStream_t st) {
-  return p.has_res2 ? pick_nw<CIN, BN, true>(p, st) : pick_nw<CIN, BN, false>(p, st);
+int pick_res(XP p, hipStream_t st) {
+  if (p.has_res2) return launch<CIN, BN, 2, 8, 2>(p, st);
+  if (p.has_res) return launch<CIN, BN, 2, 8, 1>(p, st);
+  return launch<CIN, BN, 2, 8, 0>(p, st);
 }
 
+// n-block: the whole cout when it is 32 or 48 channels, else 64-, 48- or
+// 32-channel blocks.  64-channel blocks with residuals would need more than
+// the 256 registers of two waves per SIMD (scripts/isa_probe.sh: spills, and
+// a spill's scratch traffic would break the per-stage vmcnt accounting), so
+// those layers take 32-channel blocks
 template <int CIN>
 int pick_bn(XP p, hipStream_t st) {
-  if (p.cout % 48 == 0 && p.cout <= 48) return pick_r2<CIN, 48>(p, st);
-  if (p.cout % 64 == 0) return pick_r2<CIN, 64>(p, st);
-  if (p.cout % 48 == 0) return pick_r2<CIN, 48>(p, st);
-  if (p.cout % 32 == 0) return pick_r2<CIN, 32>(p, st);
+  if (p.cout == 32 || p.cout == 48) return p.cout == 32 ? pick_res<CIN, 32>(p, st) : pick_res<CIN, 48>(p, st);
+  if (p.cout % 64 == 0 && !p.has_res) return launch<CIN, 64, 2, 8, 0>(p, st);
+  if (p.cout % 48 == 0) return pick_res<CIN, 48>(p, st);
+  if (p.cout % 32 == 0) return pick_res<CIN, 32>(p, st);
   return DCVC_HIP_EUNSUPPORTED;
 }
 
@@ -594,7 +651,6 @@ extern "C" int dcvc_internal_set_option_split(const char *name, int value) {
   else return DCVC_HIP_EINVAL;
   return DCVC_HIP_OK;
 }
-extern "C" void dcvc_internal_xconv_waves(int v) { g_nw = v; }
 
 // 3x3 stride-1 f16x3 convolutions with fp32 views (dcvc_internal_sconv calls
 // this first).  DCVC_HIP_EUNSUPPORTED: a shape / view without an
@@ -646,6 +702,7 @@ extern "C" int dcvc_internal_xconv(const dcvc_conv_args *a, void *stream) {
     p.has_res2 = 1;
     ok = ok && a->res2.dtype == DCVC_F32 && p.r2cs % 4 == 0 && p.r2co % 4 == 0 && (uintptr_t)p.res2 % 16 == 0;
   }
+  if (p.has_res2 && !p.has_res) return DCVC_HIP_EUNSUPPORTED;
   if (!ok) return DCVC_HIP_EUNSUPPORTED;
   // per-tile buffer offsets stay below 2^31 bytes
   if ((int64_t)16 * p.Wo * std::max(p.ycs, std::max(p.rcs, p.r2cs)) * 4 >= ((int64_t)1 << 30))
@@ -662,7 +719,8 @@ extern "C" int dcvc_internal_xconv(const dcvc_conv_args *a, void *stream) {
   }
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
 #ifdef XCONV_ISA_PROBE
-  return pick_bn<48>(p, st);   // (ISA inspection builds: one channel count)
+  // (ISA inspection builds, scripts/isa_probe.sh: one channel count, n-block and residual count)
+  return launch<XCONV_ISA_PROBE, XCONV_PROBE_BN, 2, 8, XCONV_PROBE_NRES>(p, st);
 #else
   switch (a->cin) {
     case 32: return pick_bn<32>(p, st);
@@ -671,6 +729,7 @@ extern "C" int dcvc_internal_xconv(const dcvc_conv_args *a, void *stream) {
     case 80: return pick_bn<80>(p, st);
     case 96: return pick_bn<96>(p, st);
     case 128: return pick_bn<128>(p, st);
+    case 192: return pick_bn<192>(p, st);
     default: return DCVC_HIP_EUNSUPPORTED;
   }
 #endif

@@ -20,9 +20,18 @@ for o in "$@"; do
   "$B/llvm-objcopy" --dump-section .hip_fatbin="$T/$n.fat" "$o"
   "$B/clang-offload-bundler" --unbundle --type=o --targets=hipv4-amdgcn-amd-amdhsa--gfx950 \
     --input="$T/$n.fat" --output="$T/$n.co"
-  c=$("$B/llvm-objdump" -d "$T/$n.co" | grep -cE "v_pk_(mul|add|fma)_f32" || true)
+  "$B/llvm-objdump" -d "$T/$n.co" > "$T/$n.s"
+  c=$(grep -cE "v_pk_(mul|add|fma)_f32" "$T/$n.s" || true)
   if [ "$c" != "0" ]; then
     echo "check_isa: $o has $c packed-f32 instructions" >&2
+    bad=1
+  fi
+  # xconv3_kernel counts its vector-memory operations per stage for exact
+  # vmcnt waits (xconv.hip): a register spill's scratch traffic would break
+  # that count, so no instantiation may spill
+  s=$(awk '/^[0-9a-f]+ <.*xconv3_kernel/{k=1; next} /^[0-9a-f]+ </{k=0} k && /scratch_/' "$T/$n.s" | wc -l)
+  if [ "$s" != "0" ]; then
+    echo "check_isa: $o has $s scratch instructions in xconv3_kernel instantiations" >&2
     bad=1
   fi
 done

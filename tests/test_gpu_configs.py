@@ -1,15 +1,17 @@
 """BASELINE.json configurations at full size on the GPU, in the bench's
-precision (Precision.fast(): bf16 feature convs, fp32 entropy-parameter
-tail): config C2 (DCVC-HEM 1920x1080, zero pad to 1088), C3 (DCVC-DC RGB
-1920x1080, replicate pad) and C4 (DCVC-DC YUV420 3840x2160, coded as YCbCr
-4:4:4), each an I-frame and two P-frames through encode_decode(...,
-output_path) as bench.py runs them.
+precision (Precision.split(): fp32 feature maps and latents, every conv on
+split-fp16 MFMA) and in the bf16 Precision.fast() kept for comparison: config
+C2 (DCVC-HEM 1920x1080, zero pad to 1088), C3 (DCVC-DC RGB 1920x1080,
+replicate pad) and C4 (DCVC-DC YUV420 3840x2160, coded as YCbCr 4:4:4), each
+an I-frame and two P-frames through encode_decode(..., output_path) as
+bench.py runs them (in split precision encode_decode also checks the fp16
+range guard, dcvc_split_range_flag).
 
 Size-independent properties checked per frame: the decoder reads back exactly
 the symbols and CDF indexes the encoder wrote (lossless round trip through the
 file), bits equal the file size, and the reconstruction and its PSNR (the
 harness's in-place clamp + squared-error kernels) are finite.  Oracle parity at full
-size is tests/test_gpu_parity_strict.py::test_strict_parity_c3_1080p.
+size is tests/test_gpu_parity_strict.py (C3, C2, and the C4 path at 1080p).
 """
 import math
 import os
@@ -31,8 +33,9 @@ def _gpu():
 CONFIGS = {"C2": ("hem", False, 1080, 1920), "C3": ("dc", False, 1080, 1920), "C4": ("dc", True, 2160, 3840)}
 
 
+@pytest.mark.parametrize("prec", ["split", "fast"])
 @pytest.mark.parametrize("cfg", ["C3", "C2", "C4"])
-def test_full_size_lossless(cfg):
+def test_full_size_lossless(cfg, prec):
     import bench
     from dcvc_amd.harness import FrameStage, psnr_rgb, psnr_yuv
     from dcvc_amd.layers import Precision
@@ -46,8 +49,8 @@ def test_full_size_lossless(cfg):
         qi, qmv, qy = bench.hem_q(isd, psd, 0)
     else:
         from dcvc_amd.dc import DMC, IntraNoAR
-    inet = IntraNoAR(precision=Precision.fast()).load_state_dict(isd)
-    pnet = DMC(precision=Precision.fast()).load_state_dict(psd)
+    inet = IntraNoAR(precision=getattr(Precision, prec)()).load_state_dict(isd)
+    pnet = DMC(precision=getattr(Precision, prec)()).load_state_dict(psd)
     inet.update(force=True)
     pnet.update(force=True)
     stage = FrameStage(h, w, 64 if hem else 16, yuv, zero_pad=hem, frame_num=3, device=dev)

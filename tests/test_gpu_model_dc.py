@@ -209,15 +209,16 @@ def run_product_estimate(dc_golden, tag, prec):
     return out
 
 
-@pytest.mark.parametrize("mode", ["parity", "fast"])
+@pytest.mark.parametrize("mode", ["split", "parity", "fast"])
 @pytest.mark.parametrize("tag", ["B", "A"])
 def test_estimate_mode_vs_reference(dc_golden, oracle_est, tag, mode):
     """Estimate mode (forward_one_frame / IntraNoAR.forward) on the GPU:
     estimated bits against the reference's own numbers (golden fixtures),
-    reconstruction PSNR against the pinned oracle."""
+    reconstruction PSNR against the pinned oracle.  split (the bench's
+    precision) and parity are held to PARITY_TOL, fast (bf16) to FAST_TOL."""
     from dcvc_amd.layers import Precision
-    prec = Precision.parity() if mode == "parity" else Precision.fast()
-    tol = PARITY_TOL if mode == "parity" else FAST_TOL
+    prec = getattr(Precision, mode)()
+    tol = FAST_TOL if mode == "fast" else PARITY_TOL
     prod = run_product_estimate(dc_golden, tag, prec)
     stats = []
     for t, (a, b) in enumerate(zip(prod, oracle_est[tag])):

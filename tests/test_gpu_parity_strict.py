@@ -179,6 +179,37 @@ def test_strict_parity_c3small_survey_recipe(prec):
             assert st["bits"] == want, msg
 
 
+@pytest.mark.parametrize("prec", ["split"])
+def test_strict_parity_c4_yuv420(prec):
+    """The C4 path (DCVC-DC on YUV420 input, test_video.py:110-195 with
+    src_type yuv420: 4:2:0 planes upsampled to 4:4:4 YCbCr and replicate-padded
+    on the GPU) at 1920x1080 in the bench's split precision: the GPU-converted
+    input equals the oracle's conversion bit for bit, then an I-frame and a
+    P-frame are held to the strict bar.  (The 4K size of C4 runs lossless in
+    tests/test_gpu_configs.py; its oracle would take minutes per frame.)"""
+    import bench
+    from dcvc_amd.harness import FrameStage
+    from dcvc_amd.synth import moving_pattern_yuv420
+    from oracle.harness_oracle import yuv_u8_to_input
+    isd, psd = bench.make_weights(None, 0, torch.device("cpu"), "dc")
+    h, w = 1080, 1920
+    H, W = 1088, 1920
+    dev = torch.device("cuda", 0)
+    stage = FrameStage(h, w, 16, True, zero_pad=False, frame_num=2, device=dev)
+    frames = []
+    for t in range(2):
+        y, uv = moving_pattern_yuv420(h, w, t, seed=1)
+        xo = torch.from_numpy(yuv_u8_to_input(y, uv, H, W)).permute(2, 0, 1).unsqueeze(0).contiguous()
+        xg = stage.load((torch.from_numpy(y).to(dev), torch.from_numpy(uv).to(dev)))
+        xg = xg.nchw() if hasattr(xg, "nchw") else xg
+        assert torch.equal(xg.float().cpu(), xo), "GPU YUV420 -> 4:4:4 input differs from the oracle's"
+        frames.append((xo[:, :, :h, :w], xo))
+    pair = Pair(isd, psd, prec)
+    stats = run_teacher_forced(pair, frames, 0, h, w, f"C4path_yuv420_1080p_{prec}")
+    for st, msg in stats:
+        print(msg)
+
+
 class HemPair(Pair):
     """DCVC-HEM: oracle/hem_oracle.py and dcvc_amd.hem in parity precision;
     one headerless int32 stream per frame (the reference's
@@ -278,7 +309,27 @@ def test_strict_parity_hem(tag, prec):
         print(msg)
 
 
-def test_hem_c1_estimate_teacher_forced():
+@pytest.mark.parametrize("prec", ["split"])
+def test_strict_parity_hem_c2_1080p(prec):
+    """Config C2 at full size (DCVC-HEM, 1920x1080 zero-padded to 1088, the
+    bench's weights, frames and rate point 0): I-frame + P-frame, teacher
+    forced, in the bench's split precision."""
+    import bench
+    from dcvc_amd.synth import moving_pattern, to_float
+    isd, psd = bench.make_weights(None, 0, torch.device("cpu"), "hem")
+    h, w = 1080, 1920
+    frames = []
+    for t in range(2):
+        x = torch.from_numpy(to_float(moving_pattern(h, w, t, seed=1))).unsqueeze(0)
+        frames.append((x, torch.nn.functional.pad(x, (0, 0, 0, 8), mode="constant", value=0)))
+    pair = HemPair(isd, psd, bench.hem_q(isd, psd, 0), prec)
+    stats = run_teacher_forced(pair, frames, None, h, w, f"hem_C2_1080p_{prec}")
+    for st, msg in stats:
+        print(msg)
+
+
+@pytest.mark.parametrize("prec", PRECS)
+def test_hem_c1_estimate_teacher_forced(prec):
     """Config C1 in estimate mode (encode_decode(output_path=None), all four
     frames, IP=4): each P-frame from the oracle's dpb (the oracle reproduces
     the reference's estimate mode bit for bit, tests/test_oracle_hem.py);
@@ -286,7 +337,7 @@ def test_hem_c1_estimate_teacher_forced():
     from tests.hem_fixtures import HEMGolden
     g = HEMGolden()
     meta = g.meta["C1"]
-    pair = HemPair(g.i_state_dict(), g.p_state_dict(), g.q("C1"))
+    pair = HemPair(g.i_state_dict(), g.p_state_dict(), g.q("C1"), prec)
     qi, qmv, qy = g.q("C1")
     dpb_o, rows = None, []
     with torch.no_grad():

@@ -46,7 +46,7 @@ def run(h, cw, x, out, opts, **kw):
         return h.lib().dcvc_last_kernel().decode()
     finally:
         for k in opts:
-            h.set_option(k, 1 if k == "xconv" else 8)
+            h.set_option(k, 1)
 
 
 # cin, cout, H, W, residual, second residual, in_op leaky ReLU
@@ -68,9 +68,8 @@ CASES = [
 ]
 
 
-@pytest.mark.parametrize("waves", [8, 4])
 @pytest.mark.parametrize("case", CASES)
-def test_xconv_matches_sconv_and_fp64(case, waves):
+def test_xconv_matches_sconv_and_fp64(case):
     h = K()
     cin, cout, H, W, res, res2, lrelu = case
     g = torch.Generator().manual_seed(cin * 7 + cout + H)
@@ -95,7 +94,7 @@ def test_xconv_matches_sconv_and_fp64(case, waves):
               in_op=h.IN_LRELU if lrelu else h.IN_NONE, in_slope=0.01,
               res=h.from_nchw(r, h.F32) if res else None, res2=h.from_nchw(r2, h.F32) if res2 else None)
     outs = []
-    for opts in ({"xconv": 1, "xconv_waves": waves}, {"xconv": 0}):
+    for opts in ({"xconv": 1}, {"xconv": 0}):
         out = h.empty(H, W, cout + 12, h.F32)
         out.buf.fill_(7.0)
         kern = run(h, cw, xa, out.ch(4, cout), opts, **kw)

@@ -190,10 +190,12 @@ def _oracle_sequence(i, p, xps, h, w, q):
 
 
 @gpu
-def test_run_test_yuv420_matches_oracle(dc_golden):
-    """A YUV420 sequence (the C4 path at 100x130) through run_test in parity
-    precision: bits and PSNR_y/u/v against the oracle codec on the same
-    4:4:4 input, within the parity tolerance of tests/test_gpu_model_dc.py."""
+@pytest.mark.parametrize("prec", ["split", "parity"])
+def test_run_test_yuv420_matches_oracle(dc_golden, prec):
+    """A YUV420 sequence (the C4 path at 100x130) through run_test in the
+    bench's split precision and in fp32: bits and PSNR_y/u/v against the
+    oracle codec on the same 4:4:4 input, within the parity tolerance of
+    tests/test_gpu_model_dc.py."""
     _need_gpu()
     from dcvc_amd.dc import DMC, IntraNoAR
     from dcvc_amd.harness import run_test, ArrayReader
@@ -204,8 +206,8 @@ def test_run_test_yuv420_matches_oracle(dc_golden):
     from tests.test_gpu_model_dc import PARITY_TOL
     h, w, n, q = 100, 130, 3, 0
     frames = [moving_pattern_yuv420(h, w, t, seed=5) for t in range(n)]
-    inet = IntraNoAR(precision=Precision.parity()).load_state_dict(dc_golden.i_state_dict())
-    pnet = DMC(precision=Precision.parity()).load_state_dict(dc_golden.p_state_dict())
+    inet = IntraNoAR(precision=getattr(Precision, prec)()).load_state_dict(dc_golden.i_state_dict())
+    pnet = DMC(precision=getattr(Precision, prec)()).load_state_dict(dc_golden.p_state_dict())
     inet.update(force=True)
     pnet.update(force=True)
     with tempfile.TemporaryDirectory() as td:
