@@ -9,6 +9,10 @@ HIPCC    ?= /opt/rocm/bin/hipcc
 # -fno-slp-vectorize: no packed-f32 VALU instructions in the kernels
 # (scripts/check_isa.sh explains why and enforces it)
 HIPFLAGS ?= -fno-slp-vectorize
+# make XCONV_DBG=1: xconv.hip with its timing-ablation switches (diagnostics only)
+ifdef XCONV_DBG
+HIPFLAGS += -DXCONV_DBG
+endif
 CXX      ?= g++
 CC       ?= gcc
 ARCH     ?= gfx950

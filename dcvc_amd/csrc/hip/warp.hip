@@ -110,6 +110,32 @@ __global__ void warp8_kernel(View x, View f, View y, const float *gx, const floa
   *reinterpret_cast<u16x8 *>(reinterpret_cast<uint16_t *>(y.p) + pix * y.cs + y.co + c) = o;
 }
 
+// The same for fp32 maps with 4-channel-aligned views: one thread per
+// (pixel, 4 channels), 16-byte corner loads and one 16-byte store (Precision.
+// split() keeps every feature map in fp32).  Same per-channel arithmetic.
+__global__ void __launch_bounds__(256) warp4_kernel(View x, View f, View y, const float *gx, const float *gy) {
+  const int q4 = y.C >> 2;
+  const int64_t t = xcd_band(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
+  const int64_t pix = t / q4;
+  if (pix >= (int64_t)y.H * y.W) return;
+  const int c = (int)(t - pix * q4) * 4;
+  const int py = (int)(pix / y.W), px = (int)(pix - (int64_t)py * y.W);
+  const float2 fv = *reinterpret_cast<const float2 *>(reinterpret_cast<const float *>(f.p) + pix * f.cs + f.co);
+  const Bilin b = warp_coords(gx[px], gy[py], fv.x, fv.y, x.W, x.H);
+  const float *xp = reinterpret_cast<const float *>(x.p) + x.co + c;
+  const int64_t r0 = (int64_t)b.y0 * x.W, r1 = (int64_t)b.y1 * x.W;
+  const float4 a = *reinterpret_cast<const float4 *>(xp + (r0 + b.x0) * x.cs);
+  const float4 bb = *reinterpret_cast<const float4 *>(xp + (r0 + b.x1) * x.cs);
+  const float4 cc = *reinterpret_cast<const float4 *>(xp + (r1 + b.x0) * x.cs);
+  const float4 d = *reinterpret_cast<const float4 *>(xp + (r1 + b.x1) * x.cs);
+  float4 o;
+  o.x = a.x * b.nw + bb.x * b.ne + cc.x * b.sw + d.x * b.se;
+  o.y = a.y * b.nw + bb.y * b.ne + cc.y * b.sw + d.y * b.se;
+  o.z = a.z * b.nw + bb.z * b.ne + cc.z * b.sw + d.z * b.se;
+  o.w = a.w * b.nw + bb.w * b.ne + cc.w * b.sw + d.w * b.se;
+  *reinterpret_cast<float4 *>(reinterpret_cast<float *>(y.p) + pix * y.cs + y.co + c) = o;
+}
+
 // bilinear x2 upsample value of channel c at full-res pixel (oy, ox) from a
 // half-res map (align_corners=False, UpSampleKernel.cpp cpu_upsample_linear)
 template <typename T>
@@ -159,6 +185,24 @@ __device__ __forceinline__ void sample3_bf16(const View &x, const Bilin &b, int 
       q[k][1] = bf2f((uint16_t)(w.hi & 0xffffu));
       q[k][2] = bf2f((uint16_t)(w.hi >> 16));
     }
+  }
+#pragma unroll
+  for (int c = 0; c < 3; ++c) v[c] = q[0][c] * b.nw + q[1][c] * b.ne + q[2][c] * b.sw + q[3][c] * b.se;
+}
+
+// fp32 features: three consecutive channels per corner in one 12-byte load
+struct __attribute__((aligned(4))) f32x3a4 { float a, b, c; };
+__device__ __forceinline__ void sample3_f32(const View &x, const Bilin &b, int c0, float v[3]) {
+  const float *base = reinterpret_cast<const float *>(x.p) + x.co + c0;
+  const int64_t r0 = (int64_t)b.y0 * x.W, r1 = (int64_t)b.y1 * x.W;
+  const int64_t e[4] = {(r0 + b.x0) * x.cs, (r0 + b.x1) * x.cs, (r1 + b.x0) * x.cs, (r1 + b.x1) * x.cs};
+  float q[4][3];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const f32x3a4 w = *reinterpret_cast<const f32x3a4 *>(base + e[k]);
+    q[k][0] = w.a;
+    q[k][1] = w.b;
+    q[k][2] = w.c;
   }
 #pragma unroll
   for (int c = 0; c < 3; ++c) v[c] = q[0][c] * b.nw + q[1][c] * b.ne + q[2][c] * b.sw + q[3][c] * b.se;
@@ -228,7 +272,12 @@ __global__ void __launch_bounds__(256) offset_div_kernel(View feat, View offs, V
     const float msk = sigmoidf_(ov[4 + k]);
     const Bilin b = warp_coords(gx[px], gy[py], dx, dy, feat.W, feat.H);
     const int src_group = i & 15;                  // x.repeat(2,1,1,1)
-    if constexpr (PAIRED) {
+    if constexpr (sizeof(TF) == 4) {
+      float v3[3];
+      sample3_f32(feat, b, 3 * src_group, v3);
+#pragma unroll
+      for (int c = 0; c < 3; ++c) xm[3 * k + c] = v3[c] * msk;
+    } else if constexpr (PAIRED) {
       float v3[3];
       if (k == 0)
         sample3_bf16<0>(feat, b, 3 * src_group, v3);  // src_group = 2g mod 16: even
@@ -333,6 +382,15 @@ extern "C" int dcvc_flow_warp(dcvc_tensor x, dcvc_tensor flow, dcvc_tensor y, co
       ((uintptr_t)x.ptr & 15) == 0 && ((uintptr_t)y.ptr & 15) == 0 && ((uintptr_t)flow.ptr & 7) == 0) {
     const int64_t total = (int64_t)y.H * y.W * (y.C / 8);
     hipLaunchKernelGGL(warp8_kernel, dim3((unsigned)((total + 255) / 256 + 7) & ~7u), dim3(256), 0, st, mk(x), mk(flow),
+                       mk(y), gx, gy);
+    DCVC_LAUNCH_CHECK();
+    return DCVC_HIP_OK;
+  }
+  if (x.dtype == DCVC_F32 && y.dtype == DCVC_F32 && y.C % 4 == 0 && x.cstride % 4 == 0 && x.coff % 4 == 0 &&
+      y.cstride % 4 == 0 && y.coff % 4 == 0 && flow.cstride % 2 == 0 && flow.coff % 2 == 0 &&
+      ((uintptr_t)x.ptr & 15) == 0 && ((uintptr_t)y.ptr & 15) == 0 && ((uintptr_t)flow.ptr & 7) == 0) {
+    const int64_t total = (int64_t)y.H * y.W * (y.C / 4);
+    hipLaunchKernelGGL(warp4_kernel, dim3((unsigned)((total + 255) / 256 + 7) & ~7u), dim3(256), 0, st, mk(x), mk(flow),
                        mk(y), gx, gy);
     DCVC_LAUNCH_CHECK();
     return DCVC_HIP_OK;

@@ -14,8 +14,9 @@
 //
 //   stage = one K step of 32 (one tap of a 32-channel chunk, or 2 / 4 packed
 //           taps of a 16- / 8-channel last chunk), one workgroup barrier;
-//   weights: streamed through a ring of four LDS slots by LDS-DMA, issued
-//           three stages ahead (L2-resident: every tile reads the same weights);
+//   weights: streamed through a ring of LDS slots by LDS-DMA, issued as many
+//           stages ahead as the ring is deep (8 to 12 slots; L2-resident:
+//           every tile reads the same weights);
 //   operands: the next stage's A (weights) and B (image) fragments are read
 //           from LDS while the current stage's MFMAs run (two register sets),
 //           so no wave waits on LDS latency at a stage start;
@@ -62,6 +63,7 @@ struct XP {
   const float *bias;
   const float *scale;
   int *ovf;               // fp16 range guard (split.h SplitRange)
+  int dbg;                // timing ablations (dcvc_set_option("xconv_dbg")), 0 in production
 };
 
 template <typename F, int... I>
@@ -90,13 +92,6 @@ struct XG {
   static constexpr int WST = BN * 32;                       // halves per weight stage (hi or lo)
   static constexpr int NDMA = 2 * BN / 16;                  // 1-KiB LDS-DMA pieces per stage
   static constexpr int DPW = (NDMA + NW - 1) / NW;          // ... per wave (every wave issues DPW)
-  // weight ring: NSW slots, the DMA of a stage issued AH = NSW - 1 stages ahead
-  static constexpr int NSW = 4, AH = NSW - 1;
-  // LDS (halves): [2 image buffers][hi, lo][IMG] | [NSW weight slots][hi, lo][WST] | DMA sink 512 | consts
-  static constexpr int L_W = 4 * IMG;
-  static constexpr int L_SINK = L_W + 2 * NSW * WST;
-  static constexpr int L_C = L_SINK + 512;
-  static constexpr size_t lds(int cout) { return (size_t)L_C * 2 + (size_t)2 * cout * 4; }
   // vector-memory instructions per thread: image chunk loads, tile loads (res, res2), epilogue stores
   static constexpr int NIMG = 2 * PPM;
   static constexpr int NTILE = NRES * RW * NT;
@@ -113,11 +108,44 @@ struct XG {
   // their DMA was issued by stage s + 2 - AH (of this tile or the previous
   // one, the schedule repeats per tile); the operations issued after it may
   // stay in flight (vmcnt counts them in issue order)
-  static constexpr int wait_n(int s) {
-    int n = after_dma((s + 2 - AH + 2 * NST) % NST);
-    for (int k = 1; k < AH - 1; ++k) n += all_ops((s + 2 - AH + k + 2 * NST) % NST);
+  static constexpr int wait_for(int s, int ah) {
+    int n = after_dma((s + 2 - ah + 2 * NST) % NST);
+    for (int k = 1; k < ah - 1; ++k) n += all_ops((s + 2 - ah + k + 2 * NST) % NST);
     return n;
   }
+  // weight ring: NSW slots, the DMA of a stage issued AH = NSW - 1 stages
+  // ahead; as many slots as the LDS holds beside the image buffers (at most a
+  // tile's stages + 1).  vmcnt completes in issue order, so every image /
+  // residual load and output store issued before a weight DMA has to land
+  // before that DMA is waited for: a deep ring gives them AH - 1 stages (the
+  // HBM latency under load), not the one or two a shallow ring would.
+  // One workgroup per CU: 8 waves of 2 rows (two waves per SIMD, 256
+  // registers each) or 4 waves of 4 rows (one wave per SIMD, 512 registers)
+  static constexpr int WPC = 1;                              // workgroups per CU
+  static constexpr int WPE = NW == 4 ? 1 : 2;                // waves per SIMD
+  static constexpr int LDS_WG = 160 * 1024 / WPC;
+  static constexpr int NSW_FIT = (LDS_WG - 2048 - 4 * IMG * 2 - 1024) / (2 * WST * 2);
+  // the deepest ring that fits, has at most a tile's stages + 1 slots and
+  // keeps every stage's count of younger vector-memory operations below 64
+  // (vmcnt is 6 bits)
+  static constexpr int pick_nsw() {
+    int n = NSW_FIT < 12 ? NSW_FIT : 12;
+    if (n > NST + 1) n = NST + 1;
+    for (; n > 4; --n) {
+      int worst = 0;
+      for (int x = 0; x < NST; ++x) worst = wait_for(x, n - 1) > worst ? wait_for(x, n - 1) : worst;
+      if (worst < 64) break;
+    }
+    return n;
+  }
+  static constexpr int NSW = pick_nsw(), AH = NSW - 1;
+  static_assert(NSW >= 4, "weight ring too shallow");
+  // LDS (halves): [2 image buffers][hi, lo][IMG] | [NSW weight slots][hi, lo][WST] | DMA sink 512 | consts
+  static constexpr int L_W = 4 * IMG;
+  static constexpr int L_SINK = L_W + 2 * NSW * WST;
+  static constexpr int L_C = L_SINK + 512;
+  static constexpr size_t lds(int cout) { return (size_t)L_C * 2 + (size_t)2 * cout * 4; }
+  static constexpr int wait_n(int s) { return wait_for(s, AH); }
 };
 
 // stage s of a tile -> (chunk, row of the chunk)
@@ -127,9 +155,15 @@ template <int KT, int CH>
 __host__ __device__ constexpr int st_row(int s) { return s - st_chunk<KT, CH>(s) * KT; }
 
 template <int CIN, int BN, int RW, int NW, int NRES>
-__global__ void __launch_bounds__(NW * 64) xconv3_kernel(XP p) {
+__global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 4 ? 1 : 2, NW == 4 ? 1 : 2)))
+xconv3_kernel(XP p) {
   typedef XG<CIN, BN, RW, NW, NRES> G;
   SplitRange rg(p.ovf);
+#ifdef XCONV_DBG
+  const int XDBG = p.dbg;   // timing ablations (ablation builds only)
+#else
+  constexpr int XDBG = 0;
+#endif
   constexpr int NTH = G::NTH, NT = G::NT, IH = G::IH, IW = G::IW, IWP = G::IWP, IMG = G::IMG;
   constexpr int WST = G::WST, CH = G::CH, KT = G::KT, TPKL = G::TPKL, ROWSL = G::ROWSL, NST = G::NST;
   constexpr int NDMA = G::NDMA, DPW = G::DPW, PPF = G::PPF, PPL = G::PPL, PPM = G::PPM;
@@ -193,6 +227,7 @@ __global__ void __launch_bounds__(NW * 64) xconv3_kernel(XP p) {
     constexpr int c = decltype(C_)::value;
     constexpr bool last = c == CH - 1;
     constexpr int PP = last ? PPL : PPF, NTOT = last ? NTOTL : NTOTF;
+    if (XDBG & 64) return;
     const int iy0 = ti.oy0 - 1, ix0 = ti.ox0 - 1;
     const int rb = iy0 > 0 ? iy0 : 0;
     const int64_t eb = (int64_t)rb * p.W * p.xcs + p.xco + c * 32;
@@ -278,6 +313,11 @@ __global__ void __launch_bounds__(NW * 64) xconv3_kernel(XP p) {
   int wcb = (int)(p.wchunk * 2), wrb = p.cout * 64;   // bytes per full chunk, per kernel row (hi or lo block)
   auto dma_w = [&](int n0, const int (&dv)[DPW], auto s_, int ws) {
     constexpr int s = decltype(s_)::value;
+    // one piece per wave: the waves past the stage's pieces issue nothing
+    // (their vmcnt waits then only cover their own register loads, which the
+    // compiler waits for at their use); with several pieces per wave every
+    // wave issues DPW (the surplus into the sink) to keep its count exact
+    if (DPW == 1 && wave >= NDMA) return;
     constexpr int c = st_chunk<KT, CH>(s), rr = st_row<KT, CH>(s);
     constexpr int rows = c == CH - 1 ? ROWSL : KT;
 #pragma unroll
@@ -309,15 +349,23 @@ __global__ void __launch_bounds__(NW * 64) xconv3_kernel(XP p) {
   }
   const int sub = hi / (4 / TPKL);
 
-  // operand registers: one set of weight fragments (each refilled with the
-  // next stage's fragment right after its last MFMA of this stage) and two
-  // sets of image fragments (the next stage's read at the stage start)
-  f16x8 oa[NT][2], ob[2][RW][2];   // [frag][hi, lo], [set][frag][hi, lo]
-  // LDS -> registers: weight fragment j of stage s (weight slot ws)
-  auto read_a = [&](int j, int ws) {
-    const uint16_t *Lw = L + G::L_W + ws * 2 * WST + aoff + j * 512;
-    oa[j][0] = *reinterpret_cast<const f16x8 *>(Lw);
-    oa[j][1] = *reinterpret_cast<const f16x8 *>(Lw + WST);
+  // operand registers: two sets of image fragments and, where the registers
+  // allow it (at most one residual, and no 64-channel block with two waves
+  // per SIMD: scripts/isa_probe.sh), two sets of weight fragments; the next
+  // stage's are read at the start of a stage, so no LDS latency is left to
+  // wait for at its end.  With one weight set, each fragment is refilled with
+  // the next stage's right after its last MFMA of the stage
+  constexpr bool DBA = NRES < 2 && (RW == 4 || BN < 64);
+  f16x8 oa[DBA ? 2 : 1][NT][2], ob[2][RW][2];   // [set][frag][hi, lo]
+  // LDS -> registers: the weight fragments of a stage (weight slot ws) into set S
+  auto read_a = [&](auto S_, int ws) {
+    constexpr int S = DBA ? decltype(S_)::value : 0;
+    const uint16_t *Lw = L + G::L_W + ws * 2 * WST + aoff;
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      oa[S][j][0] = *reinterpret_cast<const f16x8 *>(Lw + j * 512);
+      oa[S][j][1] = *reinterpret_cast<const f16x8 *>(Lw + j * 512 + WST);
+    }
   };
   // LDS -> registers: the image fragments of stage s (image buffer ib) into set S
   auto read_b = [&](auto S_, auto s_, int ib) {
@@ -353,20 +401,23 @@ __global__ void __launch_bounds__(NW * 64) xconv3_kernel(XP p) {
   };
 
   f32x4 am[RW][NT], ac[RW][NT];
-  // the MFMAs of a stage (image set S), weight fragment by weight fragment;
-  // after fragment j's last MFMA its registers take the next stage's fragment
-  // j from weight slot wsn
+  // the MFMAs of a stage (operand set S); with one weight set, fragment j is
+  // refilled from weight slot wsn after its last MFMA
   auto mfmas = [&](auto S_, int wsn) {
-    constexpr int S = decltype(S_)::value;
+    constexpr int S = decltype(S_)::value, SA = DBA ? S : 0;
 #pragma unroll
     for (int j = 0; j < NT; ++j) {
 #pragma unroll
       for (int r = 0; r < RW; ++r) {
-        am[r][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(oa[j][0], ob[S][r][0], am[r][j], 0, 0, 0);
-        ac[r][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(oa[j][0], ob[S][r][1], ac[r][j], 0, 0, 0);
-        ac[r][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(oa[j][1], ob[S][r][0], ac[r][j], 0, 0, 0);
+        am[r][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(oa[SA][j][0], ob[S][r][0], am[r][j], 0, 0, 0);
+        ac[r][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(oa[SA][j][0], ob[S][r][1], ac[r][j], 0, 0, 0);
+        ac[r][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(oa[SA][j][1], ob[S][r][0], ac[r][j], 0, 0, 0);
       }
-      read_a(j, wsn);
+      if constexpr (!DBA) {
+        const uint16_t *Lw = L + G::L_W + wsn * 2 * WST + aoff + j * 512;
+        oa[0][j][0] = *reinterpret_cast<const f16x8 *>(Lw);
+        oa[0][j][1] = *reinterpret_cast<const f16x8 *>(Lw + WST);
+      }
     }
   };
 
@@ -384,6 +435,7 @@ __global__ void __launch_bounds__(NW * 64) xconv3_kernel(XP p) {
   f32x4 rv1[NRES >= 1 ? RW : 1][NT], rv2[NRES >= 2 ? RW : 1][NT];
   auto load_res = [&](const TI &ti) {
     if constexpr (NRES == 0) return;
+    if (XDBG & 128) return;
     const int64_t rowb = (int64_t)ti.oy0 * p.Wo;
     const __amdgpu_buffer_rsrc_t r1 = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<float *>(p.res + rowb * p.rcs + p.rco), (short)0, 0x7fff0000, 0x00020000);
@@ -469,7 +521,7 @@ __global__ void __launch_bounds__(NW * 64) xconv3_kernel(XP p) {
       for (int j = 0; j < NT; ++j) {
         const bool ok = full || piece_ok(ti, r, j);
         const int o = ok ? ((px + r * p.Wo) * p.ycs + n + j * 16) * 4 : 0x7ffffff0;
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, v[r][j]), yr, o, 0, 0);
+        if (!(XDBG & 128)) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, v[r][j]), yr, o, 0, 0);
       }
   };
 
@@ -488,8 +540,7 @@ __global__ void __launch_bounds__(NW * 64) xconv3_kernel(XP p) {
   publish(0, std::integral_constant<int, 0>{});   // (waits for its own loads, so for every DMA before them)
   wait_vm_lgkm();
   __syncthreads();
-#pragma unroll
-  for (int j = 0; j < NT; ++j) read_a(j, 0);
+  read_a(std::integral_constant<int, 0>{}, 0);
   read_b(std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{}, 0);
 
   int kw = 0;   // weight slot of the current stage (stage counter mod NSW)
@@ -537,8 +588,10 @@ __global__ void __launch_bounds__(NW * 64) xconv3_kernel(XP p) {
       for (int dx = 0; dx < 3; ++dx) opaque_v(bo1[dx]), opaque_v(bo2[dx]);
       const int wsa = kw + AH >= NSW ? kw + AH - NSW : kw + AH;
       // 1. weights of stage s + AH (this tile or the next) into slot kw + AH
-      if constexpr (s + AH < NST) dma_w(tc.n0, dvc, std::integral_constant<int, (s + AH) % NST>{}, wsa);
-      else dma_w(tx.n0, dvx, std::integral_constant<int, (s + AH) % NST>{}, wsa);
+      if (!(XDBG & 8)) {
+        if constexpr (s + AH < NST) dma_w(tc.n0, dvc, std::integral_constant<int, (s + AH) % NST>{}, wsa);
+        else dma_w(tx.n0, dvx, std::integral_constant<int, (s + AH) % NST>{}, wsa);
+      }
       // 2. the next chunk's image pieces (first stage of a chunk)
       if constexpr (rr == 0) {
         if constexpr (c + 1 < CH) load_img(tc, std::integral_constant<int, (c + 1 < CH ? c + 1 : 0)>{});
@@ -552,13 +605,23 @@ __global__ void __launch_bounds__(NW * 64) xconv3_kernel(XP p) {
       constexpr int s1 = s + 1 < NST ? s + 1 : 0;
       constexpr int c1 = st_chunk<KT, CH>(s1);
       const int ib1 = (s + 1 < NST ? (c1 == c ? q : q ^ 1) : q ^ 1);
-      if constexpr (!late) read_b(std::integral_constant<int, S ^ 1>{}, std::integral_constant<int, s1>{}, ib1);
-      // 5. MFMAs of stage s (each weight fragment refilled with stage s + 1's)
-      mfmas(std::integral_constant<int, S>{}, ws1);
-      if constexpr (late) read_b(std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{}, ib1);
+      if constexpr (!late) {
+        if constexpr (DBA)
+          if (!(XDBG & 1)) read_a(std::integral_constant<int, S ^ 1>{}, ws1);
+        if (!(XDBG & 32)) read_b(std::integral_constant<int, S ^ 1>{}, std::integral_constant<int, s1>{}, ib1);
+      }
+      // 5. MFMAs of stage s (the operand reads above stay ahead of them: the
+      // scheduler would otherwise sink them to the stage's end, to reuse the
+      // registers of this stage's operands, and expose their latency)
+      sched_fence();
+      if (!(XDBG & 1)) mfmas(std::integral_constant<int, S>{}, ws1);
+      if constexpr (late) {
+        if constexpr (DBA) read_a(std::integral_constant<int, 0>{}, ws1);
+        read_b(std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{}, ib1);
+      }
       // 6. the next chunk's image into the other buffer (second-to-last stage
       // of a chunk: visible at the last stage, whose operand reads need it)
-      if constexpr (rr == rows - 2) {
+      if (rr == rows - 2 && !(XDBG & 16)) {
         if constexpr (c + 1 < CH) publish(q ^ 1, std::integral_constant<int, (c + 1 < CH ? c + 1 : 0)>{});
         else publish(q ^ 1, std::integral_constant<int, 0>{});
       }
@@ -566,16 +629,20 @@ __global__ void __launch_bounds__(NW * 64) xconv3_kernel(XP p) {
       if constexpr (s == NST - 1) epilogue(tc);
       // end of stage: stage s + 2's weights must have landed, every
       // vector-memory operation issued after their DMA may stay in flight
+      // (fenced: the scheduler would hoist the wait above the MFMAs, right
+      // behind the operand reads it would then wait for)
+      sched_fence();
       {
         constexpr int N = G::wait_n(s);
         static_assert(N < 64, "too many vector-memory operations in flight for vmcnt");
-        wait_vm_n_lgkm<N>();
+        if (XDBG & 4) wait_lgkm();
+        else wait_vm_n_lgkm<N>();
       }
       // nothing of one stage is scheduled into another: the MFMAs of a stage
       // stay between its operand reads and its barrier, so operand and
       // accumulator registers live one stage long
       sched_fence();
-      raw_barrier();
+      if (!(XDBG & 2)) raw_barrier();
       sched_fence();
       if constexpr (rr == rows - 1) q ^= 1;
       kw = kw + 1 >= NSW ? 0 : kw + 1;
@@ -586,12 +653,18 @@ __global__ void __launch_bounds__(NW * 64) xconv3_kernel(XP p) {
 
 int g_cus = 0;
 int g_enable = 1;   // dcvc_set_option("xconv", 0): route every split conv to sconv.hip
+// dcvc_set_option("xconv_dbg", bits) in builds with -DXCONV_DBG (make
+// XCONV_DBG=1): timing ablations, wrong results: 1 no MFMAs,
+// 2 no stage barrier, 4 no weight-DMA wait, 8 no weight DMA, 16 no image
+// publish, 32 no image-operand reads, 64 no image loads, 128 no residual loads
+// and output stores
+int g_dbg = 0;
 
 template <int CIN, int BN, int RW, int NW, int NRES>
 int launch(XP p, hipStream_t st) {
   typedef XG<CIN, BN, RW, NW, NRES> G;
   const size_t lds = G::lds(p.cout);
-  if (lds > 160 * 1024) return DCVC_HIP_EUNSUPPORTED;
+  if (lds > (size_t)G::LDS_WG) return DCVC_HIP_EUNSUPPORTED;
   p.tiles_x = (p.Wo + 15) / 16;
   const int tiles_y = (p.Ho + G::TH - 1) / G::TH;
   p.nblk = (p.cout + BN - 1) / BN;
@@ -606,7 +679,7 @@ int launch(XP p, hipStream_t st) {
       return DCVC_HIP_ELAUNCH;
     g_cus = prop.multiProcessorCount;
   }
-  int64_t grid = g_cus;
+  int64_t grid = (int64_t)g_cus * G::WPC;
   if (grid > nt) grid = nt;
   auto kern = xconv3_kernel<CIN, BN, RW, NW, NRES>;
   dcvc_note_kernel("xconv3_kernel<%d, %d, %d, %d, %d>@%lld", CIN, BN, RW, NW, NRES, (long long)grid * NW * 64);
@@ -616,25 +689,26 @@ int launch(XP p, hipStream_t st) {
   return DCVC_HIP_OK;
 }
 
-// the residual count picks the instantiation; 8 waves of 2 output rows each
-template <int CIN, int BN>
+// the residual count picks the instantiation
+template <int CIN, int BN, int RW, int NW>
 int pick_res(XP p, hipStream_t st) {
-  if (p.has_res2) return launch<CIN, BN, 2, 8, 2>(p, st);
-  if (p.has_res) return launch<CIN, BN, 2, 8, 1>(p, st);
-  return launch<CIN, BN, 2, 8, 0>(p, st);
+  if (p.has_res2) return launch<CIN, BN, RW, NW, 2>(p, st);
+  if (p.has_res) return launch<CIN, BN, RW, NW, 1>(p, st);
+  return launch<CIN, BN, RW, NW, 0>(p, st);
 }
 
 // n-block: the whole cout when it is 32 or 48 channels, else 64-, 48- or
-// 32-channel blocks.  64-channel blocks with residuals would need more than
-// the 256 registers of two waves per SIMD (scripts/isa_probe.sh: spills, and
-// a spill's scratch traffic would break the per-stage vmcnt accounting), so
-// those layers take 32-channel blocks
+// 32-channel blocks.  64-channel blocks with residuals would spill
+// (scripts/isa_probe.sh; a spill's scratch traffic would break the per-stage
+// vmcnt accounting), so those layers take 48- or 32-channel blocks.  8 waves
+// of 2 rows each (two waves per SIMD): 4 waves of 4 rows (one wave per SIMD,
+// 512 registers) measured 3-8 % slower (profiles/r04_xconv_ab.jsonl)
 template <int CIN>
 int pick_bn(XP p, hipStream_t st) {
-  if (p.cout == 32 || p.cout == 48) return p.cout == 32 ? pick_res<CIN, 32>(p, st) : pick_res<CIN, 48>(p, st);
+  if (p.cout == 32 || p.cout == 48) return p.cout == 32 ? pick_res<CIN, 32, 2, 8>(p, st) : pick_res<CIN, 48, 2, 8>(p, st);
   if (p.cout % 64 == 0 && !p.has_res) return launch<CIN, 64, 2, 8, 0>(p, st);
-  if (p.cout % 48 == 0) return pick_res<CIN, 48>(p, st);
-  if (p.cout % 32 == 0) return pick_res<CIN, 32>(p, st);
+  if (p.cout % 48 == 0) return pick_res<CIN, 48, 2, 8>(p, st);
+  if (p.cout % 32 == 0) return pick_res<CIN, 32, 2, 8>(p, st);
   return DCVC_HIP_EUNSUPPORTED;
 }
 
@@ -648,6 +722,7 @@ extern "C" void dcvc_internal_sconv_rw(int v);
 extern "C" int dcvc_internal_set_option_split(const char *name, int value) {
   if (std::strcmp(name, "sconv_dbg") == 0) dcvc_internal_sconv_dbg(value);
   else if (std::strcmp(name, "sconv_rw") == 0) dcvc_internal_sconv_rw(value);
+  else if (std::strcmp(name, "xconv_dbg") == 0) g_dbg = value;
   else return DCVC_HIP_EINVAL;
   return DCVC_HIP_OK;
 }
@@ -666,6 +741,7 @@ extern "C" int dcvc_internal_xconv(const dcvc_conv_args *a, void *stream) {
   if (a->in_op == DCVC_IN_LRELU && !(a->in_slope >= 0.f && a->in_slope <= 1.f)) return DCVC_HIP_EUNSUPPORTED;
   XP p{};
   p.ovf = dcvc_internal_split_flag();
+  p.dbg = g_dbg;
   p.x = reinterpret_cast<const float *>(a->x.ptr);
   p.H = a->x.H;
   p.W = a->x.W;
@@ -720,7 +796,7 @@ extern "C" int dcvc_internal_xconv(const dcvc_conv_args *a, void *stream) {
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
 #ifdef XCONV_ISA_PROBE
   // (ISA inspection builds, scripts/isa_probe.sh: one channel count, n-block and residual count)
-  return launch<XCONV_ISA_PROBE, XCONV_PROBE_BN, 2, 8, XCONV_PROBE_NRES>(p, st);
+  return launch<XCONV_ISA_PROBE, XCONV_PROBE_BN, XCONV_PROBE_RW, 8 / (XCONV_PROBE_RW / 2), XCONV_PROBE_NRES>(p, st);
 #else
   switch (a->cin) {
     case 32: return pick_bn<32>(p, st);

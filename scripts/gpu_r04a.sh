@@ -14,3 +14,9 @@ for o in "xconv=0" "xconv=1"; do
   timeout -k 10 200 python -u scripts/sconv_bench.py --reps 20 --shapes $SH --opt $o >> gpurun_out/r04a_ab.jsonl 2>&1 || exit 1
 done
 cut -c1-200 gpurun_out/r04a_ab.jsonl
+rm -f gpurun_out/r04a_abl.jsonl
+for d in; do
+  timeout -k 10 120 python -u scripts/sconv_bench.py --reps 10 --shapes 48x48@1088x1920k3r,96x48@1088x1920k3 --opt xconv_dbg=$d >> gpurun_out/r04a_abl.jsonl 2>&1 || exit 1
+done
+grep shape gpurun_out/r04a_abl.jsonl | cut -c1-200
+timeout -k 10 300 python -u -m pytest tests/test_gpu_kernels.py -q -k "warp or offset_div" --timeout 120 --timeout-method thread > gpurun_out/r04a_warp.log 2>&1; rc=$?; tail -3 gpurun_out/r04a_warp.log; [ $rc -le 1 ] || exit $rc

@@ -1,6 +1,7 @@
 """Average every PMC counter per kernel over the rocprofv3 passes under DIR
 (scripts/pmc_shape.sh) and print one JSON line per kernel with a few derived
-ratios (MFMA busy fraction, LDS bank-conflict share, wait share)."""
+ratios (MFMA busy fraction of the XCD-corrected active cycles, LDS bank-conflict
+share, wait share)."""
 import collections
 import csv
 import glob
@@ -22,7 +23,11 @@ def main(d):
         out.update({k: round(v, 1) for k, v in sorted(m.items())})
         g = m.get("GRBM_GUI_ACTIVE")
         if g and "SQ_VALU_MFMA_BUSY_CYCLES" in m:
-            out["mfma_busy_frac"] = round(m["SQ_VALU_MFMA_BUSY_CYCLES"] / (g * 256 * 4), 3)
+            # rocprofv3 sums GRBM_GUI_ACTIVE over the 8 XCDs (MI355X_MICROARCH.md,
+            # DVFS note): the kernel's cycles are g / 8; MFMA busy counts cycles
+            # summed over all 1024 SIMDs
+            out["gui_cycles"] = round(g / 8, 1)
+            out["mfma_busy_frac"] = round(m["SQ_VALU_MFMA_BUSY_CYCLES"] / (g / 8 * 256 * 4), 3)
         if "SQ_WAVE_CYCLES" in m and "SQ_WAIT_ANY" in m:
             out["wait_any_frac"] = round(m["SQ_WAIT_ANY"] / m["SQ_WAVE_CYCLES"], 3)
         if "SQ_LDS_IDX_ACTIVE" in m and "SQ_LDS_BANK_CONFLICT" in m and m["SQ_LDS_IDX_ACTIVE"]:

@@ -226,6 +226,31 @@ def test_flow_warp_bf16_vector_path():
     assert (got == ref).float().mean().item() > 0.99
 
 
+def test_flow_warp_f32_vector_path_bit_identical():
+    """fp32 maps with 4-channel-aligned views take the 16-byte-per-corner
+    kernel (warp4_kernel); a view at an odd channel offset takes the scalar
+    kernel: the same per-channel arithmetic, so identical bits, and the
+    reference formula within fp32 rounding."""
+    from oracle.dc_oracle import flow_warp
+    h = K()
+    H, W = 37, 61
+    x = torch.randn(1, 56, H, W)
+    flow = torch.randn(1, 2, H, W) * 6
+    xa = to_act(x, h.F32)
+    fa = to_act(flow, h.F32)
+    y4 = h.empty(H, W, 56, h.F32)
+    y1 = h.empty(H, W, 56, h.F32)
+    y4.buf.fill_(3.0)
+    h.flow_warp(xa.ch(4, 48), fa, _grid(H, W), y=y4.ch(4, 48))
+    h.flow_warp(xa.ch(4, 48), fa, _grid(H, W), y=y1.ch(5, 48))   # odd output offset: scalar kernel
+    torch.cuda.synchronize()
+    got4 = back(y4)[:, 4:52]
+    assert torch.equal(got4, back(y1)[:, 5:53])
+    assert bool((back(y4)[:, :4] == 3.0).all()) and bool((back(y4)[:, 52:] == 3.0).all())
+    ref = flow_warp(x[:, 4:52], flow)
+    assert (got4 - ref).abs().max().item() < 1e-5
+
+
 def test_resize_and_pool():
     from oracle.dc_oracle import up2, down2
     h = K()

@@ -37,6 +37,9 @@ def rel_err(got, ref):
     return (got.double() - ref).abs().max().item() / scale
 
 
+DEFAULTS = {"xconv": 1}
+
+
 def run(h, cw, x, out, opts, **kw):
     for k, v in opts.items():
         h.set_option(k, v)
@@ -46,7 +49,7 @@ def run(h, cw, x, out, opts, **kw):
         return h.lib().dcvc_last_kernel().decode()
     finally:
         for k in opts:
-            h.set_option(k, 1)
+            h.set_option(k, DEFAULTS[k])
 
 
 # cin, cout, H, W, residual, second residual, in_op leaky ReLU
