@@ -63,6 +63,7 @@ struct XP {
   const float *bias;
   const float *scale;
   int *ovf;               // fp16 range guard (split.h SplitRange)
+  int shuffle;            // pixel-shuffled output (r = 2)
   int dbg;                // timing ablations (dcvc_set_option("xconv_dbg")), 0 in production
 };
 
@@ -154,10 +155,11 @@ __host__ __device__ constexpr int st_chunk(int s) { return s < (CH - 1) * KT ? s
 template <int KT, int CH>
 __host__ __device__ constexpr int st_row(int s) { return s - st_chunk<KT, CH>(s) * KT; }
 
-template <int CIN, int BN, int RW, int NW, int NRES>
+template <int CIN, int BN, int RW, int NW, int NRES, bool SHUF>
 __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 4 ? 1 : 2, NW == 4 ? 1 : 2)))
 xconv3_kernel(XP p) {
   typedef XG<CIN, BN, RW, NW, NRES> G;
+  static_assert(!SHUF || NRES == 0, "pixel-shuffle outputs take no residuals");
   SplitRange rg(p.ovf);
 #ifdef XCONV_DBG
   const int XDBG = p.dbg;   // timing ablations (ablation builds only)
@@ -183,7 +185,8 @@ xconv3_kernel(XP p) {
   // bias / scale of every output channel, once
   for (int i = tid; i < p.cout; i += NTH) {
     Lc[i] = p.bias ? p.bias[i] : 0.f;
-    Lc[p.cout + i] = p.scale ? p.scale[i] : 1.f;
+    // (with pixel shuffle the scale is per output channel, cout / 4 of them)
+    Lc[p.cout + i] = p.scale && i < (SHUF ? p.cout >> 2 : p.cout) ? p.scale[i] : 1.f;
   }
 
   // ---- image piece plan.  Piece u of a chunk with NS staged 8-channel slots
@@ -486,6 +489,47 @@ xconv3_kernel(XP p) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) v[r][j][e] = fmaxf(v[r][j][e], v[r][j][e] * p.slope);
     }
+    if constexpr (SHUF) {
+      // pixel shuffle (r = 2): conv channel 4 c + 2 dy + dx of pixel (oy, ox)
+      // is output channel c of pixel (2 oy + dy, 2 ox + dx).  Lane row hi
+      // holds conv channels n0 + 16 j + 4 hi + e (e = 2 dy + dx): a 4 x 4
+      // transpose across the rows (v_permlane32_swap, then v_permlane16_swap)
+      // gives row hi the 4 consecutive output channels (n0 + 16 j) / 4 + e of
+      // sub-pixel hi, one 16-byte store; then the output-channel scale
+      const __amdgpu_buffer_rsrc_t ys = __builtin_amdgcn_make_buffer_rsrc(
+          p.y + (int64_t)(2 * ti.oy0) * (2 * p.Wo) * p.ycs + p.yco, (short)0, 0x7fff0000, 0x00020000);
+#pragma unroll
+      for (int r = 0; r < RW; ++r)
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+          // (__float_as_uint: hipcc's __builtin_bit_cast of a vector element
+          // reads element 0 whatever the index)
+          uint32_t x0 = __float_as_uint(v[r][j][0]), x1 = __float_as_uint(v[r][j][1]);
+          uint32_t x2 = __float_as_uint(v[r][j][2]), x3 = __float_as_uint(v[r][j][3]);
+#ifdef __HIP_DEVICE_COMPILE__
+          const auto a02 = __builtin_amdgcn_permlane32_swap(x0, x2, false, false);
+          const auto a13 = __builtin_amdgcn_permlane32_swap(x1, x3, false, false);
+          const auto b01 = __builtin_amdgcn_permlane16_swap(a02[0], a13[0], false, false);
+          const auto b23 = __builtin_amdgcn_permlane16_swap(a02[1], a13[1], false, false);
+          x0 = b01[0];
+          x1 = b01[1];
+          x2 = b23[0];
+          x3 = b23[1];
+#endif
+          const int cb = (ti.n0 >> 2) + 4 * j;
+          const float4 sc = *reinterpret_cast<const float4 *>(Lc + p.cout + cb);
+          f32x4 o;
+          o[0] = __uint_as_float(x0) * sc.x;
+          o[1] = __uint_as_float(x1) * sc.y;
+          o[2] = __uint_as_float(x2) * sc.z;
+          o[3] = __uint_as_float(x3) * sc.w;
+          const int ry = 2 * (wave * RW + r) + (hi >> 1), cx = 2 * (ti.ox0 + col) + (hi & 1);
+          const bool ok = ti.oy0 + wave * RW + r < p.Ho && ti.ox0 + col < p.Wo && ti.n0 + 16 * j < p.cout;
+          const int off = ok ? ((ry * 2 * p.Wo + cx) * p.ycs + cb) * 4 : 0x7ffffff0;
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, o), ys, off, 0, 0);
+        }
+      return;
+    }
     if constexpr (NRES >= 1) {
 #pragma unroll
       for (int r = 0; r < RW; ++r)
@@ -660,7 +704,7 @@ int g_enable = 1;   // dcvc_set_option("xconv", 0): route every split conv to sc
 // and output stores
 int g_dbg = 0;
 
-template <int CIN, int BN, int RW, int NW, int NRES>
+template <int CIN, int BN, int RW, int NW, int NRES, bool SHUF = false>
 int launch(XP p, hipStream_t st) {
   typedef XG<CIN, BN, RW, NW, NRES> G;
   const size_t lds = G::lds(p.cout);
@@ -681,8 +725,9 @@ int launch(XP p, hipStream_t st) {
   }
   int64_t grid = (int64_t)g_cus * G::WPC;
   if (grid > nt) grid = nt;
-  auto kern = xconv3_kernel<CIN, BN, RW, NW, NRES>;
-  dcvc_note_kernel("xconv3_kernel<%d, %d, %d, %d, %d>@%lld", CIN, BN, RW, NW, NRES, (long long)grid * NW * 64);
+  auto kern = xconv3_kernel<CIN, BN, RW, NW, NRES, SHUF>;
+  dcvc_note_kernel("xconv3_kernel<%d, %d, %d, %d, %d, %s>@%lld", CIN, BN, RW, NW, NRES, SHUF ? "shuf" : "",
+                   (long long)grid * NW * 64);
   dcvc_ensure_lds(reinterpret_cast<const void *>(kern), 160 * 1024);
   hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(NW * 64), lds, st, p);
   DCVC_LAUNCH_CHECK();
@@ -705,6 +750,11 @@ int pick_res(XP p, hipStream_t st) {
 // 512 registers) measured 3-8 % slower (profiles/r04_xconv_ab.jsonl)
 template <int CIN>
 int pick_bn(XP p, hipStream_t st) {
+  if (p.shuffle) {   // no residuals, cout % 16 == 0 (dcvc_internal_xconv)
+    if (p.cout % 64 == 0) return launch<CIN, 64, 2, 8, 0, true>(p, st);
+    if (p.cout % 48 == 0) return launch<CIN, 48, 2, 8, 0, true>(p, st);
+    return launch<CIN, 32, 2, 8, 0, true>(p, st);
+  }
   if (p.cout == 32 || p.cout == 48) return p.cout == 32 ? pick_res<CIN, 32, 2, 8>(p, st) : pick_res<CIN, 48, 2, 8>(p, st);
   if (p.cout % 64 == 0 && !p.has_res) return launch<CIN, 64, 2, 8, 0>(p, st);
   if (p.cout % 48 == 0) return pick_res<CIN, 48, 2, 8>(p, st);
@@ -732,7 +782,10 @@ extern "C" int dcvc_internal_set_option_split(const char *name, int value) {
 // instantiation, left to sconv.hip.
 extern "C" int dcvc_internal_xconv(const dcvc_conv_args *a, void *stream) {
   if (!g_enable) return DCVC_HIP_EUNSUPPORTED;
-  if (a->kh != 3 || a->kw != 3 || a->stride != 1 || a->pad != 1 || a->shuffle) return DCVC_HIP_EUNSUPPORTED;
+  if (a->kh != 3 || a->kw != 3 || a->stride != 1 || a->pad != 1) return DCVC_HIP_EUNSUPPORTED;
+  // pixel shuffle: whole 16-channel groups (4 output channels per lane after
+  // the epilogue's transpose), no residuals
+  if (a->shuffle && (a->cout % 16 || a->res.ptr || a->res2.ptr)) return DCVC_HIP_EUNSUPPORTED;
   if (a->in_op != DCVC_IN_NONE && a->in_op != DCVC_IN_LRELU) return DCVC_HIP_EUNSUPPORTED;
   if (a->x.dtype != DCVC_F32 || a->y.dtype != DCVC_F32) return DCVC_HIP_EUNSUPPORTED;
   // leaky ReLUs are computed as max(v, slope v): exact for 0 <= slope <= 1
@@ -760,7 +813,8 @@ extern "C" int dcvc_internal_xconv(const dcvc_conv_args *a, void *stream) {
   p.slope = a->slope;
   p.bias = a->bias;
   p.scale = a->scale;
-  if (a->y.W != p.Wo || a->y.H != p.Ho) return DCVC_HIP_EUNSUPPORTED;
+  p.shuffle = a->shuffle ? 1 : 0;
+  if (a->y.W != (a->shuffle ? 2 : 1) * p.Wo || a->y.H != (a->shuffle ? 2 : 1) * p.Ho) return DCVC_HIP_EUNSUPPORTED;
   // 16-byte pieces everywhere: input slots of 8 channels, output / residual pieces of 4
   bool ok = a->cin % 8 == 0 && p.xcs % 4 == 0 && p.xco % 4 == 0 && (uintptr_t)p.x % 16 == 0;
   ok = ok && a->cout % 4 == 0 && p.ycs % 4 == 0 && p.yco % 4 == 0 && (uintptr_t)p.y % 16 == 0;

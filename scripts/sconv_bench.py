@@ -3,7 +3,7 @@
     python scripts/sconv_bench.py [--reps 20] [--shapes 48x48@1088x1920k3r,...] [--opt NAME=VALUE]
 
 A shape is CINxCOUT@HxW then kK (kernel size, default 3), sS (stride,
-default 1) and "r" for an fp32 residual input.  One JSON line per shape:
+default 1), "r" for an fp32 residual input and "u" for a pixel-shuffled output.  One JSON line per shape:
 kernel, us/launch, algorithmic GB/s (fp32 input, split weights, output,
 residual once each) and fp32-equivalent TFLOP/s (against 2500/3 = 833 peak).
 """
@@ -35,22 +35,23 @@ def main():
         name, val = o.split("=")
         K.set_option(name, int(val))
     for sh in a.shapes.split(","):
-        m = re.fullmatch(r"(\d+)x(\d+)@(\d+)x(\d+)(?:k(\d))?(?:s(\d))?(r?)", sh)
+        m = re.fullmatch(r"(\d+)x(\d+)@(\d+)x(\d+)(?:k(\d))?(?:s(\d))?(r?)(u?)", sh)
         cin, cout, H, W = (int(m.group(i)) for i in range(1, 5))
         k = int(m.group(5) or 3)
         s = int(m.group(6) or 1)
         res = m.group(7) == "r"
+        shuf = m.group(8) == "u"
         cw = K.ConvW(torch.randn(cout, cin, k, k) / (cin * k * k) ** 0.5, torch.randn(cout) * 0.1, s, K.F16X3, dev)
         x = K.from_nchw(torch.randn(1, cin, H, W, device=dev), K.F32)
         Ho, Wo = cw.out_hw(H, W)
         r = K.from_nchw(torch.randn(1, cout, Ho, Wo, device=dev), K.F32) if res else None
-        y = K.empty(Ho, Wo, cout, K.F32, dev)
+        y = K.empty(Ho * 2, Wo * 2, cout // 4, K.F32, dev) if shuf else K.empty(Ho, Wo, cout, K.F32, dev)
         for _ in range(3):
-            K.conv(cw, x, y, act=K.ACT_LRELU, slope=0.1, res=r)
+            K.conv(cw, x, y, act=K.ACT_LRELU, slope=0.1, res=r, shuffle=shuf)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         for _ in range(a.reps):
-            K.conv(cw, x, y, act=K.ACT_LRELU, slope=0.1, res=r)
+            K.conv(cw, x, y, act=K.ACT_LRELU, slope=0.1, res=r, shuffle=shuf)
         e1.record()
         torch.cuda.synchronize()
         us = e0.elapsed_time(e1) * 1e3 / a.reps

@@ -127,3 +127,49 @@ def test_xconv_repeatable_under_load():
         h.conv(cw, x, y0)
     torch.cuda.synchronize()
     assert torch.equal(y0.buf, ref)
+
+
+# cin, cout, H, W, leaky ReLU, scale (pixel-shuffle layers: subpel_conv3x3 of
+# DCVC-DC/src/models/video_net.py:40-45 and the UNet / context up paths)
+SHUF_CASES = [
+    (128, 192, 34, 60, True, False),
+    (96, 256, 17, 31, False, True),     # ragged tiles, output-channel scale
+    (64, 64, 20, 22, False, False),
+    (192, 128, 9, 40, True, True),
+    (32, 80, 19, 21, True, False),      # a half-filled last n-block
+]
+
+
+@pytest.mark.parametrize("case", SHUF_CASES)
+def test_xconv_pixel_shuffle(case):
+    """xconv's shuffle epilogue (4 x 4 cross-row transpose of the accumulator
+    pieces) against sconv's LDS-staged one (identical bits) and fp64; output
+    into a channel view, nothing written outside it."""
+    h = K()
+    cin, cout, H, W, lrelu, scaled = case
+    g = torch.Generator().manual_seed(cin + cout + H)
+    x = torch.randn(1, cin, H, W, generator=g)
+    w = torch.randn(cout, cin, 3, 3, generator=g) / (cin * 9) ** 0.5
+    b = torch.randn(cout, generator=g) * 0.1
+    sc = torch.rand(cout // 4, generator=g) + 0.5
+    ref = F.conv2d(x.double(), w.double(), b.double(), padding=1)
+    if lrelu:
+        ref = F.leaky_relu(ref, 0.1)
+    ref = F.pixel_shuffle(ref, 2)
+    if scaled:
+        ref = ref * sc.double().view(1, -1, 1, 1)
+    cw = h.ConvW(w, b, 1, h.F16X3)
+    xa = h.from_nchw(x, h.F32)
+    kw = dict(act=h.ACT_LRELU if lrelu else h.ACT_NONE, slope=0.1, shuffle=True,
+              scale=sc.cuda() if scaled else None)
+    co = cout // 4
+    outs = []
+    for opts in ({"xconv": 1}, {"xconv": 0}):
+        out = h.empty(2 * H, 2 * W, co + 8, h.F32)
+        out.buf.fill_(7.0)
+        kern = run(h, cw, xa, out.ch(4, co), opts, **kw)
+        assert kern.startswith("xconv3_kernel" if opts["xconv"] else "sconv_kernel"), kern
+        assert bool((out.buf[:, :, :4] == 7.0).all()) and bool((out.buf[:, :, 4 + co:] == 7.0).all())
+        outs.append(out.ch(4, co).nchw().cpu())
+    assert rel_err(outs[0], ref) < TOL
+    assert torch.equal(outs[0], outs[1])
