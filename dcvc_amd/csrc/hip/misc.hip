@@ -77,12 +77,14 @@ template <> struct V8<float> {
 
 template <typename TX, typename TY>
 __global__ void dw8_kernel(View x, View y, const float *w, const float *b) {
-  const int cg = y.C >> 3;
-  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= (int64_t)y.H * y.W * cg) return;
-  const int c = (int)(idx % cg) * 8;
-  const int64_t pix = idx / cg;
-  const int py = (int)(pix / y.W), px = (int)(pix - (int64_t)py * y.W);
+  // workgroup (x, y): 256 (pixel, 8-channel group) items of row y (32-bit
+  // index math: no 64-bit divisions per thread)
+  const unsigned cg = (unsigned)y.C >> 3;
+  const unsigned t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (unsigned)y.W * cg) return;
+  const int py = blockIdx.y, px = (int)(t / cg);
+  const int c = (int)(t - (unsigned)px * cg) * 8;
+  const int64_t pix = (int64_t)py * y.W + px;
   float acc[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) acc[j] = 0.f;
@@ -367,8 +369,8 @@ extern "C" int dcvc_dwconv3x3(dcvc_tensor x, dcvc_tensor y, const float *w, cons
   const bool vec = (x.C % 8 == 0) && (x.cstride % 8 == 0) && (x.coff % 8 == 0) && (y.cstride % 8 == 0) &&
                    (y.coff % 8 == 0);
   if (vec) {
-    const unsigned g = blocks_for((int64_t)y.H * y.W * (y.C / 8));
-#define K(TX, TY) hipLaunchKernelGGL((dw8_kernel<TX, TY>), dim3(g), dim3(256), 0, st, mk(x), mk(y), w, bias)
+    const dim3 g(blocks_for((int64_t)y.W * (y.C / 8)), (unsigned)y.H);
+#define K(TX, TY) hipLaunchKernelGGL((dw8_kernel<TX, TY>), g, dim3(256), 0, st, mk(x), mk(y), w, bias)
     DISPATCH2(x.dtype, y.dtype, K);
 #undef K
   } else {

@@ -192,10 +192,11 @@ __device__ __forceinline__ void sample3_bf16(const View &x, const Bilin &b, int 
 
 // fp32 features: three consecutive channels per corner in one 12-byte load
 struct __attribute__((aligned(4))) f32x3a4 { float a, b, c; };
+// (element offsets in 32 bits: the host checks H * W * cstride < 2^31)
 __device__ __forceinline__ void sample3_f32(const View &x, const Bilin &b, int c0, float v[3]) {
   const float *base = reinterpret_cast<const float *>(x.p) + x.co + c0;
-  const int64_t r0 = (int64_t)b.y0 * x.W, r1 = (int64_t)b.y1 * x.W;
-  const int64_t e[4] = {(r0 + b.x0) * x.cs, (r0 + b.x1) * x.cs, (r1 + b.x0) * x.cs, (r1 + b.x1) * x.cs};
+  const int r0 = b.y0 * x.W, r1 = b.y1 * x.W;
+  const int e[4] = {(r0 + b.x0) * x.cs, (r0 + b.x1) * x.cs, (r1 + b.x0) * x.cs, (r1 + b.x1) * x.cs};
   float q[4][3];
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
@@ -220,11 +221,11 @@ __global__ void __launch_bounds__(256) offset_div_kernel(View feat, View offs, V
   for (int i = threadIdx.x; i < 48 * 6; i += 256) sfw[i] = fw[i];
   if (threadIdx.x < 48) sfb[threadIdx.x] = fb[threadIdx.x];
   __syncthreads();
-  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int g = (int)(t & 15);
-  const int64_t pix = t >> 4;
-  if (pix >= (int64_t)y.H * y.W) return;
-  const int py = (int)(pix / y.W), px = (int)(pix - (int64_t)py * y.W);
+  // workgroup (x, y): pixels 16 x .. 16 x + 15 of row y, thread = 16 pixel + group
+  const int g = threadIdx.x & 15;
+  const int py = blockIdx.y, px = blockIdx.x * 16 + (threadIdx.x >> 4);
+  if (px >= y.W) return;
+  const int64_t pix = (int64_t)py * y.W + px;
   const float fx = ld<float>(flow.p, pix * flow.cs + flow.co);
   const float fy = ld<float>(flow.p, pix * flow.cs + flow.co + 1);
   // bilinear x2 upsample of the half-resolution offset map (up2_at), the
@@ -420,10 +421,10 @@ extern "C" int dcvc_offset_diversity(dcvc_tensor feat, dcvc_tensor offs, dcvc_te
   if (offs.dtype == DCVC_F32 && (offs.cstride % 4 || offs.coff % 4 || ((uintptr_t)offs.ptr & 15)))
     return DCVC_HIP_EUNSUPPORTED;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  const int64_t threads = (int64_t)y.H * y.W * 16;
-  const unsigned grd = (unsigned)((threads + 255) / 256);
+  const dim3 grd((unsigned)((y.W + 15) / 16), (unsigned)y.H);
+  if ((int64_t)feat.H * feat.W * feat.cstride >= ((int64_t)1 << 31)) return DCVC_HIP_EUNSUPPORTED;
 #define LAUNCH(TF, TO, TY, PR)                                                                  \
-  hipLaunchKernelGGL((offset_div_kernel<TF, TO, TY, PR>), dim3(grd), dim3(256), 0, st, mk(feat), \
+  hipLaunchKernelGGL((offset_div_kernel<TF, TO, TY, PR>), grd, dim3(256), 0, st, mk(feat),       \
                      mk(offs), mk(flow), mk(y), fw, fb, gx, gy, max_mag)
   const bool f32 = feat.dtype == DCVC_F32, o32 = offs.dtype == DCVC_F32, y32 = y.dtype == DCVC_F32;
   const bool paired = !f32 && feat.cstride % 2 == 0 && feat.coff % 2 == 0 && ((uintptr_t)feat.ptr & 3) == 0;

@@ -608,7 +608,8 @@ def dwconv3x3(x, w9c, b, y=None):
         y = empty(x.H, x.W, x.C, x.dtype, x.buf.device)
     e0 = _t0()
     check(lib().dcvc_dwconv3x3(x.c(), y.c(), w9c.data_ptr(), b.data_ptr(), stream()), "dwconv3x3")
-    _t1(e0, "dwconv", 18 * x.H * x.W * x.C, x.H * x.W * x.C * (_esz(x.dtype) + _esz(y.dtype)))
+    _t1(e0, "dwconv", 18 * x.H * x.W * x.C, x.H * x.W * x.C * (_esz(x.dtype) + _esz(y.dtype)),
+        f"dwconv | {x.H}x{x.W}x{x.C}")
     return y
 
 
@@ -618,7 +619,8 @@ def flow_warp(x, flow, grid, y=None):
     gx, gy = grid
     e0 = _t0()
     check(lib().dcvc_flow_warp(x.c(), flow.c(), y.c(), gx.data_ptr(), gy.data_ptr(), stream()), "flow_warp")
-    _t1(e0, "warp", 8 * y.H * y.W * y.C, y.H * y.W * (y.C * (_esz(x.dtype) + _esz(y.dtype)) + 8))
+    _t1(e0, "warp", 8 * y.H * y.W * y.C, y.H * y.W * (y.C * (_esz(x.dtype) + _esz(y.dtype)) + 8),
+        f"warp | {y.H}x{y.W}x{y.C}")
     return y
 
 
@@ -629,7 +631,8 @@ def offset_diversity(feat, offs_half, flow, fw, fb, grid, y=None, max_mag=40.0):
     e0 = _t0()
     check(lib().dcvc_offset_diversity(feat.c(), offs_half.c(), flow.c(), y.c(), fw.data_ptr(), fb.data_ptr(),
                                       gx.data_ptr(), gy.data_ptr(), max_mag, stream()), "offset_diversity")
-    _t1(e0, "offset_diversity", y.H * y.W * 48 * 20, y.H * y.W * (96 * _esz(feat.dtype) + 8))
+    _t1(e0, "offset_diversity", y.H * y.W * 48 * 20, y.H * y.W * (96 * _esz(feat.dtype) + 8),
+        f"offset_diversity | {y.H}x{y.W}")
     return y
 
 

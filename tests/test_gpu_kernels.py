@@ -179,13 +179,15 @@ def test_conv_gate_input():
     assert rel_err(back(y), ref) < 2e-5
 
 
-def test_dwconv3x3():
+@pytest.mark.parametrize("C,H,W", [(48, 17, 23), (64, 9, 200), (128, 5, 61)])
+def test_dwconv3x3(C, H, W):
+    # (64, 9, 200): several workgroups per image row (the kernel's 2D grid)
     h = K()
-    x = torch.randn(1, 48, 17, 23)
-    w = torch.randn(48, 1, 3, 3)
-    b = torch.randn(48)
-    ref = F.conv2d(x, w, b, padding=1, groups=48)
-    w9c = w.reshape(48, 9).t().contiguous().cuda()
+    x = torch.randn(1, C, H, W)
+    w = torch.randn(C, 1, 3, 3)
+    b = torch.randn(C)
+    ref = F.conv2d(x, w, b, padding=1, groups=C)
+    w9c = w.reshape(C, 9).t().contiguous().cuda()
     y = h.dwconv3x3(to_act(x, h.F32), w9c, b.cuda())
     torch.cuda.synchronize()
     assert rel_err(back(y), ref) < 1e-5
