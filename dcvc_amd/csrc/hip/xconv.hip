@@ -726,7 +726,8 @@ int launch(XP p, hipStream_t st) {
   int64_t grid = (int64_t)g_cus * G::WPC;
   if (grid > nt) grid = nt;
   auto kern = xconv3_kernel<CIN, BN, RW, NW, NRES, SHUF>;
-  dcvc_note_kernel("xconv3_kernel<%d, %d, %d, %d, %d, %s>@%lld", CIN, BN, RW, NW, NRES, SHUF ? "shuf" : "",
+  // (the name as rocprofv3 prints the instantiation: scripts/pmc_summary.py keys on it)
+  dcvc_note_kernel("xconv3_kernel<%d, %d, %d, %d, %d, %s>@%lld", CIN, BN, RW, NW, NRES, SHUF ? "true" : "false",
                    (long long)grid * NW * 64);
   dcvc_ensure_lds(reinterpret_cast<const void *>(kern), 160 * 1024);
   hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(NW * 64), lds, st, p);
