@@ -76,10 +76,12 @@ __device__ __forceinline__ void sfor(F &&f) {
   sfor_(f, std::make_integer_sequence<int, N>{});
 }
 
-template <int CIN, int BN, int RW, int NW, int NRES>
+template <int CIN, int BN, int RW, int NW, int NRES, int KS = 3>
 struct XG {
-  static constexpr int KT = 9, NTH = NW * 64, TH = NW * RW, NT = BN / 16;
-  static constexpr int IH = TH + 2, IW = 18, IWP = 20;
+  // KS x KS kernel (3 or 7), pad KS / 2: a 16-column tile reads a halo image
+  // of IH x IW pixels, rows padded to IWP (a multiple of 4 pixels, swzx)
+  static constexpr int KT = KS * KS, NTH = NW * 64, TH = NW * RW, NT = BN / 16;
+  static constexpr int IH = TH + KS - 1, IW = 15 + KS, IWP = (IW + 3) & ~3;
   static constexpr int CH = (CIN + 31) / 32;
   static constexpr int VCL = CIN - 32 * (CH - 1);
   static constexpr int TPKL = VCL <= 8 ? 4 : (VCL <= 16 ? 2 : 1);
@@ -155,11 +157,12 @@ __host__ __device__ constexpr int st_chunk(int s) { return s < (CH - 1) * KT ? s
 template <int KT, int CH>
 __host__ __device__ constexpr int st_row(int s) { return s - st_chunk<KT, CH>(s) * KT; }
 
-template <int CIN, int BN, int RW, int NW, int NRES, bool SHUF>
+template <int CIN, int BN, int RW, int NW, int NRES, bool SHUF, int KS>
 __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 4 ? 1 : 2, NW == 4 ? 1 : 2)))
 xconv3_kernel(XP p) {
-  typedef XG<CIN, BN, RW, NW, NRES> G;
+  typedef XG<CIN, BN, RW, NW, NRES, KS> G;
   static_assert(!SHUF || NRES == 0, "pixel-shuffle outputs take no residuals");
+  constexpr int PAD = KS / 2;
   SplitRange rg(p.ovf);
 #ifdef XCONV_DBG
   const int XDBG = p.dbg;   // timing ablations (ablation builds only)
@@ -231,7 +234,7 @@ xconv3_kernel(XP p) {
     constexpr bool last = c == CH - 1;
     constexpr int PP = last ? PPL : PPF, NTOT = last ? NTOTL : NTOTF;
     if (XDBG & 64) return;
-    const int iy0 = ti.oy0 - 1, ix0 = ti.ox0 - 1;
+    const int iy0 = ti.oy0 - PAD, ix0 = ti.ox0 - PAD;
     const int rb = iy0 > 0 ? iy0 : 0;
     const int64_t eb = (int64_t)rb * p.W * p.xcs + p.xco + c * 32;
     int64_t nrec = ((int64_t)p.H * p.W * p.xcs - eb) * 4;
@@ -341,9 +344,9 @@ xconv3_kernel(XP p) {
   // per-lane operand offsets (halves): weights (row j * 16 + col, slot hi)
   int aoff = swz(col, hi);
   // image, one tap per K step: pixel (wave rows + dy, col + dx), slot hi
-  int bo1[3], bo2[3];
+  int bo1[KS], bo2[KS];
 #pragma unroll
-  for (int dx = 0; dx < 3; ++dx) {
+  for (int dx = 0; dx < KS; ++dx) {
     const int x = col + dx;
     bo1[dx] = swzx(wave * RW * IWP + x, x, hi);
     // packed taps: slot hi % (4 / TPKL)
@@ -378,7 +381,7 @@ xconv3_kernel(XP p) {
     constexpr int tpk = c == CH - 1 ? TPKL : 1;
     const uint16_t *Li = L + ib * 2 * IMG;
     if constexpr (tpk == 1) {
-      constexpr int dy = rr / 3, dx = rr % 3;
+      constexpr int dy = rr / KS, dx = rr % KS;
 #pragma unroll
       for (int r = 0; r < RW; ++r) {
         const int o = bo1[dx] + (r + dy) * IWP * 32;
@@ -391,8 +394,8 @@ xconv3_kernel(XP p) {
       constexpr int ta = tpk * rr, tb = tpk * rr + 1;
       constexpr int ta_ = ta < KT ? ta : 0, tb_ = tb < KT ? tb : 0;
       static_assert(tpk == 2, "4-tap packing (<= 8-channel chunks) is not instantiated");
-      const int oA = bo2[ta_ % 3] + (ta_ / 3) * IWP * 32;
-      const int oB = bo2[tb_ % 3] + (tb_ / 3) * IWP * 32;
+      const int oA = bo2[ta_ % KS] + (ta_ / KS) * IWP * 32;
+      const int oB = bo2[tb_ % KS] + (tb_ / KS) * IWP * 32;
       const int o0 = sub ? oB : oA;
 #pragma unroll
       for (int r = 0; r < RW; ++r) {
@@ -597,7 +600,7 @@ xconv3_kernel(XP p) {
     // of hoisting dozens of them out of the tile loop into live registers
     opaque_v(aoff);
 #pragma unroll
-    for (int dx = 0; dx < 3; ++dx) opaque_v(bo1[dx]), opaque_v(bo2[dx]);
+    for (int dx = 0; dx < KS; ++dx) opaque_v(bo1[dx]), opaque_v(bo2[dx]);
 #pragma unroll
     for (int d = 0; d < DPW; ++d) opaque_v(dlane[d]), opaque_v(drow[d]);
     opaque_s(wcb);
@@ -629,7 +632,7 @@ xconv3_kernel(XP p) {
       // the same ring slot), which would keep it live in between
       opaque_v(aoff);
 #pragma unroll
-      for (int dx = 0; dx < 3; ++dx) opaque_v(bo1[dx]), opaque_v(bo2[dx]);
+      for (int dx = 0; dx < KS; ++dx) opaque_v(bo1[dx]), opaque_v(bo2[dx]);
       const int wsa = kw + AH >= NSW ? kw + AH - NSW : kw + AH;
       // 1. weights of stage s + AH (this tile or the next) into slot kw + AH
       if (!(XDBG & 8)) {
@@ -704,9 +707,9 @@ int g_enable = 1;   // dcvc_set_option("xconv", 0): route every split conv to sc
 // and output stores
 int g_dbg = 0;
 
-template <int CIN, int BN, int RW, int NW, int NRES, bool SHUF = false>
+template <int CIN, int BN, int RW, int NW, int NRES, bool SHUF = false, int KS = 3>
 int launch(XP p, hipStream_t st) {
-  typedef XG<CIN, BN, RW, NW, NRES> G;
+  typedef XG<CIN, BN, RW, NW, NRES, KS> G;
   const size_t lds = G::lds(p.cout);
   if (lds > (size_t)G::LDS_WG) return DCVC_HIP_EUNSUPPORTED;
   p.tiles_x = (p.Wo + 15) / 16;
@@ -725,9 +728,9 @@ int launch(XP p, hipStream_t st) {
   }
   int64_t grid = (int64_t)g_cus * G::WPC;
   if (grid > nt) grid = nt;
-  auto kern = xconv3_kernel<CIN, BN, RW, NW, NRES, SHUF>;
+  auto kern = xconv3_kernel<CIN, BN, RW, NW, NRES, SHUF, KS>;
   // (the name as rocprofv3 prints the instantiation: scripts/pmc_summary.py keys on it)
-  dcvc_note_kernel("xconv3_kernel<%d, %d, %d, %d, %d, %s>@%lld", CIN, BN, RW, NW, NRES, SHUF ? "true" : "false",
+  dcvc_note_kernel("xconv3_kernel<%d, %d, %d, %d, %d, %s, %d>@%lld", CIN, BN, RW, NW, NRES, SHUF ? "true" : "false", KS,
                    (long long)grid * NW * 64);
   dcvc_ensure_lds(reinterpret_cast<const void *>(kern), 160 * 1024);
   hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(NW * 64), lds, st, p);
@@ -783,7 +786,10 @@ extern "C" int dcvc_internal_set_option_split(const char *name, int value) {
 // instantiation, left to sconv.hip.
 extern "C" int dcvc_internal_xconv(const dcvc_conv_args *a, void *stream) {
   if (!g_enable) return DCVC_HIP_EUNSUPPORTED;
-  if (a->kh != 3 || a->kw != 3 || a->stride != 1 || a->pad != 1) return DCVC_HIP_EUNSUPPORTED;
+  // 3x3 (pad 1) and SpyNet's 7x7 (pad 3), stride 1
+  if (a->kh != a->kw || a->stride != 1 || !((a->kh == 3 && a->pad == 1) || (a->kh == 7 && a->pad == 3)))
+    return DCVC_HIP_EUNSUPPORTED;
+  if (a->kh == 7 && (a->shuffle || a->res.ptr)) return DCVC_HIP_EUNSUPPORTED;
   // pixel shuffle: whole 16-channel groups (4 output channels per lane after
   // the epilogue's transpose), no residuals
   if (a->shuffle && (a->cout % 16 || a->res.ptr || a->res2.ptr)) return DCVC_HIP_EUNSUPPORTED;
@@ -841,9 +847,10 @@ extern "C" int dcvc_internal_xconv(const dcvc_conv_args *a, void *stream) {
   const int nch = (a->cin + 31) / 32;
   const int vc = a->cin - 32 * (nch - 1);
   const int tpkl = vc <= 8 ? 4 : vc <= 16 ? 2 : 1;
-  p.wchunk = (int64_t)2 * 9 * a->cout * 32;
+  const int kt = a->kh * a->kw;
+  p.wchunk = (int64_t)2 * kt * a->cout * 32;
   {
-    const int rl = (9 + tpkl - 1) / tpkl;
+    const int rl = (kt + tpkl - 1) / tpkl;
     const int64_t wb = ((int64_t)(nch - 1) * p.wchunk + (int64_t)2 * rl * a->cout * 32) * 2;
     if (wb >= ((int64_t)1 << 31) - 64) return DCVC_HIP_EUNSUPPORTED;
     p.wbytes = (int)wb;
@@ -851,8 +858,22 @@ extern "C" int dcvc_internal_xconv(const dcvc_conv_args *a, void *stream) {
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
 #ifdef XCONV_ISA_PROBE
   // (ISA inspection builds, scripts/isa_probe.sh: one channel count, n-block and residual count)
-  return launch<XCONV_ISA_PROBE, XCONV_PROBE_BN, XCONV_PROBE_RW, 8 / (XCONV_PROBE_RW / 2), XCONV_PROBE_NRES>(p, st);
+  return launch<XCONV_ISA_PROBE, XCONV_PROBE_BN, XCONV_PROBE_RW, 8 / (XCONV_PROBE_RW / 2), XCONV_PROBE_NRES, false,
+                XCONV_PROBE_KS>(p, st);
 #else
+  if (a->kh == 7) {
+    // SpyNet's 7x7 layers (video_net.py:79-100): the halo image of a 22 x 22
+    // pixel tile leaves LDS for a weight ring of 16- or 32-channel blocks
+    switch (a->cin) {
+      case 16: return a->cout == 16 ? launch<16, 16, 2, 8, 0, false, 7>(p, st)
+                                    : a->cout % 32 == 0 ? launch<16, 32, 2, 8, 0, false, 7>(p, st) : DCVC_HIP_EUNSUPPORTED;
+      case 32: return a->cout == 16 ? launch<32, 16, 2, 8, 0, false, 7>(p, st)
+                                    : a->cout % 32 == 0 ? launch<32, 32, 2, 8, 0, false, 7>(p, st) : DCVC_HIP_EUNSUPPORTED;
+      case 64: return a->cout == 16 ? launch<64, 16, 2, 8, 0, false, 7>(p, st)
+                                    : a->cout % 32 == 0 ? launch<64, 32, 2, 8, 0, false, 7>(p, st) : DCVC_HIP_EUNSUPPORTED;
+      default: return DCVC_HIP_EUNSUPPORTED;
+    }
+  }
   switch (a->cin) {
     case 32: return pick_bn<32>(p, st);
     case 48: return pick_bn<48>(p, st);

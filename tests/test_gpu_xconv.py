@@ -173,3 +173,43 @@ def test_xconv_pixel_shuffle(case):
         outs.append(out.ch(4, co).nchw().cpu())
     assert rel_err(outs[0], ref) < TOL
     assert torch.equal(outs[0], outs[1])
+
+
+# cin, cout, H, W, slope (SpyNet's 7x7 basic-module convs,
+# DCVC-DC/src/models/video_net.py:79-100: ReLU = slope 0, and none on the last)
+K7_CASES = [
+    (32, 64, 40, 70, 0.0),
+    (64, 32, 37, 53, 0.0),
+    (32, 16, 21, 35, 0.0),
+    (16, 32, 18, 40, 0.1),
+    (64, 32, 136, 240, None),   # many tiles per workgroup
+]
+
+
+@pytest.mark.parametrize("case", K7_CASES)
+def test_xconv_7x7(case):
+    """7x7 stride-1 layers on the static-shape kernel: identical bits to
+    sconv's 7x7 path and fp64 within the split bound, into a channel view."""
+    h = K()
+    cin, cout, H, W, slope = case
+    g = torch.Generator().manual_seed(cin * 3 + cout + H)
+    big = torch.randn(1, cin + 8, H, W, generator=g)
+    x = big[:, 4:4 + cin]
+    w = torch.randn(cout, cin, 7, 7, generator=g) / (cin * 49) ** 0.5
+    b = torch.randn(cout, generator=g) * 0.1
+    ref = F.conv2d(x.double(), w.double(), b.double(), padding=3)
+    if slope is not None:
+        ref = F.leaky_relu(ref, slope)
+    cw = h.ConvW(w, b, 1, h.F16X3)
+    xa = h.from_nchw(big, h.F32).ch(4, cin)
+    kw = dict(act=h.ACT_LRELU if slope is not None else h.ACT_NONE, slope=slope or 0.0)
+    outs = []
+    for opts in ({"xconv": 1}, {"xconv": 0}):
+        out = h.empty(H, W, cout + 8, h.F32)
+        out.buf.fill_(7.0)
+        kern = run(h, cw, xa, out.ch(4, cout), opts, **kw)
+        assert kern.startswith("xconv3_kernel" if opts["xconv"] else "sconv_kernel"), kern
+        assert bool((out.buf[:, :, :4] == 7.0).all()) and bool((out.buf[:, :, 4 + cout:] == 7.0).all())
+        outs.append(out.ch(4, cout).nchw().cpu())
+    assert rel_err(outs[0], ref) < TOL
+    assert torch.equal(outs[0], outs[1])
