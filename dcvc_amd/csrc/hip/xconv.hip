@@ -266,19 +266,22 @@ xconv3_kernel(XP p) {
   };
   // LDS image buffer ib <- registers, split (ResBlock's leaky ReLU first:
   // lrelu(v) = max(v, slope v) for 0 <= slope <= 1)
-  auto publish = [&](int ib, auto C_) {
+  // (pieces [U0, U1) of the chunk: a chunk's publish is spread over several
+  // stages, so no stage carries all of its VALU work beside its 18 MFMAs)
+  auto publish = [&](int ib, auto C_, auto U0_, auto U1_) {
     constexpr int c = decltype(C_)::value;
     constexpr bool last = c == CH - 1;
     constexpr int PP = last ? PPL : PPF, NTOT = last ? NTOTL : NTOTF;
+    constexpr int U0 = decltype(U0_)::value, U1 = decltype(U1_)::value < PP ? decltype(U1_)::value : PP;
     uint16_t *const Lh = L + ib * 2 * IMG;
     if (p.in_lrelu) {
 #pragma unroll
-      for (int u = 0; u < PP; ++u)
+      for (int u = U0; u < U1; ++u)
 #pragma unroll
         for (int j = 0; j < 8; ++j) pf[u][j] = fmaxf(pf[u][j], pf[u][j] * p.in_slope);
     }
 #pragma unroll
-    for (int u = 0; u < PP; ++u) {
+    for (int u = U0; u < U1; ++u) {
       u32x4_t h, l;
       rg.add8(pf[u]);
       split8(pf[u], h, l);
@@ -584,7 +587,8 @@ xconv3_kernel(XP p) {
     });
     load_img(t0, std::integral_constant<int, 0>{});
   }
-  publish(0, std::integral_constant<int, 0>{});   // (waits for its own loads, so for every DMA before them)
+  publish(0, std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{},
+          std::integral_constant<int, PPF>{});   // (waits for its own loads, so for every DMA before them)
   wait_vm_lgkm();
   __syncthreads();
   read_a(std::integral_constant<int, 0>{}, 0);
@@ -666,11 +670,22 @@ xconv3_kernel(XP p) {
         if constexpr (DBA) read_a(std::integral_constant<int, 0>{}, ws1);
         read_b(std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{}, ib1);
       }
-      // 6. the next chunk's image into the other buffer (second-to-last stage
-      // of a chunk: visible at the last stage, whose operand reads need it)
-      if (rr == rows - 2 && !(XDBG & 16)) {
-        if constexpr (c + 1 < CH) publish(q ^ 1, std::integral_constant<int, (c + 1 < CH ? c + 1 : 0)>{});
-        else publish(q ^ 1, std::integral_constant<int, 0>{});
+      // 6. the next chunk's image into the other buffer, visible at the
+      // chunk's last stage, whose operand reads need it: one piece per stage
+      // up to the second-to-last stage where the chunk has room for that
+      // (the pieces loaded at its first stage), else all at the second-to-last
+      {
+        constexpr int cn = c + 1 < CH ? c + 1 : 0;
+        constexpr int PPn = cn == CH - 1 ? PPL : PPF;
+        constexpr int w0 = rows - 1 - PPn;   // the first publishing stage
+        using CN = std::integral_constant<int, cn>;
+        if constexpr (w0 >= 1) {
+          if constexpr (rr >= w0 && rr <= rows - 2)
+            if (!(XDBG & 16))
+              publish(q ^ 1, CN{}, std::integral_constant<int, rr - w0>{}, std::integral_constant<int, rr - w0 + 1>{});
+        } else if constexpr (rr == rows - 2) {
+          if (!(XDBG & 16)) publish(q ^ 1, CN{}, std::integral_constant<int, 0>{}, std::integral_constant<int, PPn>{});
+        }
       }
       // 7. epilogue
       if constexpr (s == NST - 1) epilogue(tc);
@@ -739,10 +754,14 @@ int launch(XP p, hipStream_t st) {
 }
 
 // the residual count picks the instantiation
-template <int CIN, int BN, int RW, int NW>
+template <int CIN, int BN, int RW, int NW, bool RES_OK = true>
 int pick_res(XP p, hipStream_t st) {
-  if (p.has_res2) return launch<CIN, BN, RW, NW, 2>(p, st);
-  if (p.has_res) return launch<CIN, BN, RW, NW, 1>(p, st);
+  if constexpr (RES_OK) {
+    if (p.has_res2) return launch<CIN, BN, RW, NW, 2>(p, st);
+    if (p.has_res) return launch<CIN, BN, RW, NW, 1>(p, st);
+  } else if (p.has_res) {
+    return DCVC_HIP_EUNSUPPORTED;
+  }
   return launch<CIN, BN, RW, NW, 0>(p, st);
 }
 
@@ -752,17 +771,19 @@ int pick_res(XP p, hipStream_t st) {
 // vmcnt accounting), so those layers take 48- or 32-channel blocks.  8 waves
 // of 2 rows each (two waves per SIMD): 4 waves of 4 rows (one wave per SIMD,
 // 512 registers) measured 3-8 % slower (profiles/r04_xconv_ab.jsonl)
-template <int CIN>
+// RES_OK false: no residual instantiations (80 input channels: they spill,
+// and no 80-channel layer of the codecs takes a residual)
+template <int CIN, bool RES_OK = true>
 int pick_bn(XP p, hipStream_t st) {
   if (p.shuffle) {   // no residuals, cout % 16 == 0 (dcvc_internal_xconv)
     if (p.cout % 64 == 0) return launch<CIN, 64, 2, 8, 0, true>(p, st);
     if (p.cout % 48 == 0) return launch<CIN, 48, 2, 8, 0, true>(p, st);
     return launch<CIN, 32, 2, 8, 0, true>(p, st);
   }
-  if (p.cout == 32 || p.cout == 48) return p.cout == 32 ? pick_res<CIN, 32, 2, 8>(p, st) : pick_res<CIN, 48, 2, 8>(p, st);
+  if (p.cout == 32 || p.cout == 48) return p.cout == 32 ? pick_res<CIN, 32, 2, 8, RES_OK>(p, st) : pick_res<CIN, 48, 2, 8, RES_OK>(p, st);
   if (p.cout % 64 == 0 && !p.has_res) return launch<CIN, 64, 2, 8, 0>(p, st);
-  if (p.cout % 48 == 0) return pick_res<CIN, 48, 2, 8>(p, st);
-  if (p.cout % 32 == 0) return pick_res<CIN, 32, 2, 8>(p, st);
+  if (p.cout % 48 == 0) return pick_res<CIN, 48, 2, 8, RES_OK>(p, st);
+  if (p.cout % 32 == 0) return pick_res<CIN, 32, 2, 8, RES_OK>(p, st);
   return DCVC_HIP_EUNSUPPORTED;
 }
 
@@ -878,7 +899,7 @@ extern "C" int dcvc_internal_xconv(const dcvc_conv_args *a, void *stream) {
     case 32: return pick_bn<32>(p, st);
     case 48: return pick_bn<48>(p, st);
     case 64: return pick_bn<64>(p, st);
-    case 80: return pick_bn<80>(p, st);
+    case 80: return pick_bn<80, false>(p, st);
     case 96: return pick_bn<96>(p, st);
     case 128: return pick_bn<128>(p, st);
     case 192: return pick_bn<192>(p, st);

@@ -8,9 +8,9 @@ timeout -k 10 500 python -u -m pytest tests/test_gpu_xconv.py tests/test_gpu_spl
 rc=$?; echo "xconv tests rc=$rc"; tail -15 gpurun_out/r04a_xconv_tests.log
 # a fault, abort or time limit ends the call here; ordinary test failures go on to the timing
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
-SH=48x48@1088x1920k3r,128x192@544x960k3u,32x64@1088x1920k7,64x32@1088x1920k7,32x16@1088x1920k7,32x64@544x960k7,64x32@544x960k7
+SH=48x48@1088x1920k3,48x48@1088x1920k3r,64x64@544x960k3r,96x48@1088x1920k3,128x64@544x960k3,128x192@544x960k3u,32x64@1088x1920k7
 rm -f gpurun_out/r04a_ab.jsonl
-for o in "xconv=0" "xconv=1"; do
+for o in "xconv=1"; do
   timeout -k 10 200 python -u scripts/sconv_bench.py --reps 20 --shapes $SH --opt $o >> gpurun_out/r04a_ab.jsonl 2>&1 || exit 1
 done
 cut -c1-200 gpurun_out/r04a_ab.jsonl
