@@ -277,8 +277,8 @@ __global__ void __launch_bounds__(kNT) sdc_kernel(DP p) {
         rg.add4(v);
         const auto h01 = __builtin_amdgcn_cvt_pkrtz(v[0], v[1]);
         const auto h23 = __builtin_amdgcn_cvt_pkrtz(v[2], v[3]);
-        const uint32_t l01 = pk((v[0] - (float)h01[0]) * 2048.f, (v[1] - (float)h01[1]) * 2048.f);
-        const uint32_t l23 = pk((v[2] - (float)h23[0]) * 2048.f, (v[3] - (float)h23[1]) * 2048.f);
+        const uint32_t l01 = pk(split_lo(v[0], (float)h01[0]), split_lo(v[1], (float)h01[1]));
+        const uint32_t l23 = pk(split_lo(v[2], (float)h23[0]), split_lo(v[3], (float)h23[1]));
         const int o = swz((c >> 5) * (TH * TW) + px, (c & 31) >> 3) + (c & 7);
         typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
         *reinterpret_cast<u32x2_t *>(Dh + o) = u32x2_t{__builtin_bit_cast(uint32_t, h01), __builtin_bit_cast(uint32_t, h23)};

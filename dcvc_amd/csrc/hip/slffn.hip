@@ -180,8 +180,8 @@ __global__ void __launch_bounds__(kNT) slffn_kernel(LP p) {
       rg.add4(v);
       const auto h0 = __builtin_amdgcn_cvt_pkrtz(v[0], v[1]);
       const auto h1 = __builtin_amdgcn_cvt_pkrtz(v[2], v[3]);
-      const uint32_t l0 = pk((v[0] - (float)h0[0]) * 2048.f, (v[1] - (float)h0[1]) * 2048.f);
-      const uint32_t l1 = pk((v[2] - (float)h1[0]) * 2048.f, (v[3] - (float)h1[1]) * 2048.f);
+      const uint32_t l0 = pk(split_lo(v[0], (float)h0[0]), split_lo(v[1], (float)h0[1]));
+      const uint32_t l1 = pk(split_lo(v[2], (float)h1[0]), split_lo(v[3], (float)h1[1]));
       const int off = swz((wave >> 1) * P + pb * 16 + col, (wave & 1) * 2 + (g >> 1)) + (g & 1) * 4;
       typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
       *reinterpret_cast<u32x2_t *>(Hh + off) =

@@ -33,13 +33,18 @@ __device__ __forceinline__ uint32_t pk(float a, float b) {
 // the fp16 value of v rounded toward zero (exact below fp16's normal range
 // too: the remainder is taken from hi's own fp32 value), lo = (v - hi) * 2^11
 // (v - hi is exact in fp32), rounded toward zero to fp16
+// lo of v given h = f16_rtz(v) widened: (v - h) * 2^11 as fma(h, -2^11, v 2^11),
+// the same value (both products and the difference are exact), one
+// v_fma_mix_f32 reading the f16 h directly instead of a conversion, a
+// subtraction and a multiplication
+__device__ __forceinline__ float split_lo(float v, float h) { return __builtin_fmaf(h, -2048.f, v * 2048.f); }
+
 __device__ __forceinline__ void split8(const float v[8], u32x4_t &h, u32x4_t &l) {
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const auto hh = __builtin_amdgcn_cvt_pkrtz(v[2 * j], v[2 * j + 1]);
-    const float h0 = (float)hh[0], h1 = (float)hh[1];
     h[j] = __builtin_bit_cast(uint32_t, hh);
-    l[j] = pk((v[2 * j] - h0) * 2048.f, (v[2 * j + 1] - h1) * 2048.f);
+    l[j] = pk(split_lo(v[2 * j], (float)hh[0]), split_lo(v[2 * j + 1], (float)hh[1]));
   }
 }
 
