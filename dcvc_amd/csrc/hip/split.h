@@ -33,6 +33,21 @@ __device__ __forceinline__ uint32_t pk(float a, float b) {
 // the fp16 value of v rounded toward zero (exact below fp16's normal range
 // too: the remainder is taken from hi's own fp32 value), lo = (v - hi) * 2^11
 // (v - hi is exact in fp32), rounded toward zero to fp16
+// leaky ReLU of a loaded value, 0 <= s <= 1: max(v, s v) as one v_max_f32
+// (fmaxf would first quieten v, a signalling NaN for all the compiler knows:
+// one more instruction per element); the same value for every non-NaN v,
+// signed zeros included
+__device__ __forceinline__ float lrelu_in(float v, float s) {
+  const float t = v * s;
+#ifdef __HIP_DEVICE_COMPILE__
+  float r;
+  asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(v), "v"(t));
+  return r;
+#else
+  return v > t ? v : t;
+#endif
+}
+
 // lo of v given h = f16_rtz(v) widened: (v - h) * 2^11 as fma(h, -2^11, v 2^11),
 // the same value (both products and the difference are exact), one
 // v_fma_mix_f32 reading the f16 h directly instead of a conversion, a
@@ -81,11 +96,18 @@ __device__ __forceinline__ void opaque_s(T &x) {
 // 2^15.  The store is a plain vector store of one lane per wave at most.
 constexpr float kSplitMax = 32768.f;
 struct SplitRange {
-  float m = 0.f;
+  // running max of |v| as the bit pattern of the absolute value: for
+  // non-negative floats integer order is float order, and a NaN or an
+  // infinity counts as out of range too.  Integer max3 over sign-cleared bits
+  // (v_and + v_max3_u32) instead of fmaxf, which canonicalises each input
+  uint32_t m = 0;
   int *flag;
   __device__ explicit SplitRange(int *f) : flag(f) {}
   __device__ __forceinline__ void add4(const float *v) {
-    m = fmaxf(m, fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
+    const uint32_t a = __float_as_uint(v[0]) & 0x7fffffffu, b = __float_as_uint(v[1]) & 0x7fffffffu;
+    const uint32_t c = __float_as_uint(v[2]) & 0x7fffffffu, d = __float_as_uint(v[3]) & 0x7fffffffu;
+    m = max(max(m, a), b);
+    m = max(max(m, c), d);
     // fold now: left to itself the compiler keeps every partial max live
     // until the kernel's end (tens of registers in a long unrolled kernel)
     opaque_v(m);
@@ -95,9 +117,10 @@ struct SplitRange {
     add4(v + 4);
   }
   __device__ ~SplitRange() {
-    if (flag && m >= kSplitMax) *flag = 1;
+    if (flag && m >= 0x47000000u) *flag = 1;   // 0x47000000 = kSplitMax
   }
 };
+static_assert(0x47000000u == 0x47000000u && kSplitMax == 32768.f, "2^15 is 0x47000000");
 
 __device__ __forceinline__ void wait_vm_lgkm() { __builtin_amdgcn_s_waitcnt(0x0070); }   // vmcnt(0) lgkmcnt(0)
 // vmcnt(N) lgkmcnt(0): all but the N youngest vector-memory operations done

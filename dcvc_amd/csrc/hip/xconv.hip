@@ -278,7 +278,7 @@ xconv3_kernel(XP p) {
 #pragma unroll
       for (int u = U0; u < U1; ++u)
 #pragma unroll
-        for (int j = 0; j < 8; ++j) pf[u][j] = fmaxf(pf[u][j], pf[u][j] * p.in_slope);
+        for (int j = 0; j < 8; ++j) pf[u][j] = lrelu_in(pf[u][j], p.in_slope);
     }
 #pragma unroll
     for (int u = U0; u < U1; ++u) {
