@@ -76,6 +76,12 @@ __device__ __forceinline__ void sfor(F &&f) {
   sfor_(f, std::make_integer_sequence<int, N>{});
 }
 
+#ifdef XCONV_DBG
+// per-stage clock stamps of workgroup 0's second tile (ablation builds):
+// [wave][2 * stage + {0: MFMAs issued, 1: past the barrier}], low 32 bits of s_memtime
+__device__ unsigned g_xstamps[8 * 64];
+#endif
+
 template <int CIN, int BN, int RW, int NW, int NRES, int KS = 3>
 struct XG {
   // KS x KS kernel (3 or 7), pad KS / 2: a 16-column tile reads a halo image
@@ -594,11 +600,18 @@ xconv3_kernel(XP p) {
   read_a(std::integral_constant<int, 0>{}, 0);
   read_b(std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{}, 0);
 
+#ifdef XCONV_DBG
+  unsigned stampv = 0;   // lane 2 s (+1) of one VGPR per stage stamp
+#endif
   int kw = 0;   // weight slot of the current stage (stage counter mod NSW)
   int q = 0;    // image buffer of the current chunk (chunk counter mod 2)
   for (int t = g; t < p.ntiles; t += G0) {
     const int tn = t + G0 < p.ntiles ? t + G0 : t;   // the next tile (prefetch target; itself when last)
-    const TI tc = tile_of(t), tx = tile_of(tn);
+    TI tc = tile_of(t), tx = tile_of(tn);
+    // computed once per tile: opaque, so the compiler keeps (or spills) them
+    // instead of redoing tile_of's divisions in every stage that reads them
+    opaque_s(tc.n0), opaque_s(tc.oy0), opaque_s(tc.ox0);
+    opaque_s(tx.n0), opaque_s(tx.oy0), opaque_s(tx.ox0);
     // the per-lane LDS / DMA offsets are opaque to the compiler here, so it
     // computes each stage's addresses inside the stage (an add or two) instead
     // of hoisting dozens of them out of the tile loop into live registers
@@ -661,11 +674,24 @@ xconv3_kernel(XP p) {
           if (!(XDBG & 1)) read_a(std::integral_constant<int, S ^ 1>{}, ws1);
         if (!(XDBG & 32)) read_b(std::integral_constant<int, S ^ 1>{}, std::integral_constant<int, s1>{}, ib1);
       }
-      // 5. MFMAs of stage s (the operand reads above stay ahead of them: the
-      // scheduler would otherwise sink them to the stage's end, to reuse the
-      // registers of this stage's operands, and expose their latency)
-      sched_fence();
+      // 5. MFMAs of stage s.  With two operand sets, the next stage's reads
+      // above are interleaved one per MFMA from the stage's first MFMA on
+      // (the MFMAs read the other set): no MFMA waits behind the stage's
+      // scalar work and reads, and no read is left to the stage's end (where
+      // the scheduler would sink them to reuse this stage's registers, and
+      // expose their latency).  With one set the reads stay ahead of them
+      if constexpr (!(DBA && !late)) sched_fence();
       if (!(XDBG & 1)) mfmas(std::integral_constant<int, S>{}, ws1);
+#ifdef __HIP_DEVICE_COMPILE__
+      if constexpr (DBA && !late) {
+        constexpr int NMF = 3 * RW * NT, NRD = 2 * NT + 2 * RW;
+        sfor<(NRD < NMF ? NRD : NMF)>([&](auto) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // one MFMA
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // one LDS read
+        });
+        if constexpr (NMF > NRD) __builtin_amdgcn_sched_group_barrier(0x008, NMF - NRD, 0);
+      }
+#endif
       if constexpr (late) {
         if constexpr (DBA) read_a(std::integral_constant<int, 0>{}, ws1);
         read_b(std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{}, ib1);
@@ -694,6 +720,10 @@ xconv3_kernel(XP p) {
       // (fenced: the scheduler would hoist the wait above the MFMAs, right
       // behind the operand reads it would then wait for)
       sched_fence();
+#ifdef XCONV_DBG
+      if (2 * s + 1 < 64 && t == g + G0)
+        asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(stampv) : "s"((unsigned)__builtin_amdgcn_s_memtime()), "i"(2 * s));
+#endif
       {
         constexpr int N = G::wait_n(s);
         static_assert(N < 64, "too many vector-memory operations in flight for vmcnt");
@@ -706,11 +736,18 @@ xconv3_kernel(XP p) {
       sched_fence();
       if (!(XDBG & 2)) raw_barrier();
       sched_fence();
+#ifdef XCONV_DBG
+      if (2 * s + 1 < 64 && t == g + G0)
+        asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(stampv) : "s"((unsigned)__builtin_amdgcn_s_memtime()), "i"(2 * s + 1));
+#endif
       if constexpr (rr == rows - 1) q ^= 1;
       kw = kw + 1 >= NSW ? 0 : kw + 1;
     });
   }
   wait_vm_lgkm();   // no LDS-DMA left in flight when the workgroup exits
+#ifdef XCONV_DBG
+  if (blockIdx.x == 0 && wave < 8) g_xstamps[wave * 64 + lane] = stampv;
+#endif
 }
 
 int g_cus = 0;
@@ -790,6 +827,17 @@ int pick_bn(XP p, hipStream_t st) {
 }  // namespace
 
 extern "C" void dcvc_internal_xconv_enable(int v) { g_enable = v; }
+
+// the stamps of the last launch (ablation builds; DCVC_HIP_EUNSUPPORTED otherwise)
+extern "C" int dcvc_internal_xconv_stamps(unsigned *host) {
+#ifdef XCONV_DBG
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_xstamps), sizeof(unsigned) * 8 * 64) == hipSuccess
+             ? DCVC_HIP_OK : DCVC_HIP_ELAUNCH;
+#else
+  (void)host;
+  return DCVC_HIP_EUNSUPPORTED;
+#endif
+}
 extern "C" void dcvc_internal_sconv_dbg(int v);
 extern "C" void dcvc_internal_sconv_rw(int v);
 
