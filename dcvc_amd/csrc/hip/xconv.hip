@@ -418,8 +418,34 @@ xconv3_kernel(XP p) {
   f32x4 am[RW][NT], ac[RW][NT];
   // the MFMAs of a stage (operand set S); with one weight set, fragment j is
   // refilled from weight slot wsn after its last MFMA
-  auto mfmas = [&](auto S_, int wsn) {
-    constexpr int S = decltype(S_)::value, SA = DBA ? S : 0;
+  // (PASS with two operand sets: 0 all, 1 the am pass, 2 the two ac passes)
+  auto mfmas = [&](auto S_, int wsn, auto PASS_) {
+    constexpr int S = decltype(S_)::value, SA = DBA ? S : 0, PASS = decltype(PASS_)::value;
+    if constexpr (DBA) {
+      // in three passes, so the two products accumulated into ac[r][j] are
+      // RW * NT MFMAs apart (no MFMA waits on its predecessor's result); the
+      // same accumulation order, so the same bits
+      if constexpr (PASS != 2) {
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+#pragma unroll
+          for (int r = 0; r < RW; ++r)
+            am[r][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(oa[SA][j][0], ob[S][r][0], am[r][j], 0, 0, 0);
+      }
+      if constexpr (PASS != 1) {
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+#pragma unroll
+          for (int r = 0; r < RW; ++r)
+            ac[r][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(oa[SA][j][0], ob[S][r][1], ac[r][j], 0, 0, 0);
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+#pragma unroll
+          for (int r = 0; r < RW; ++r)
+            ac[r][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(oa[SA][j][1], ob[S][r][0], ac[r][j], 0, 0, 0);
+      }
+      return;
+    }
 #pragma unroll
     for (int j = 0; j < NT; ++j) {
 #pragma unroll
@@ -651,18 +677,26 @@ xconv3_kernel(XP p) {
 #pragma unroll
       for (int dx = 0; dx < KS; ++dx) opaque_v(bo1[dx]), opaque_v(bo2[dx]);
       const int wsa = kw + AH >= NSW ? kw + AH - NSW : kw + AH;
-      // 1. weights of stage s + AH (this tile or the next) into slot kw + AH
-      if (!(XDBG & 8)) {
-        if constexpr (s + AH < NST) dma_w(tc.n0, dvc, std::integral_constant<int, (s + AH) % NST>{}, wsa);
-        else dma_w(tx.n0, dvx, std::integral_constant<int, (s + AH) % NST>{}, wsa);
-      }
-      // 2. the next chunk's image pieces (first stage of a chunk)
-      if constexpr (rr == 0) {
-        if constexpr (c + 1 < CH) load_img(tc, std::integral_constant<int, (c + 1 < CH ? c + 1 : 0)>{});
-        else load_img(tx, std::integral_constant<int, 0>{});
-      }
-      // 3. the tile's residuals
-      if constexpr (s == 0) load_res(tc);
+      // 1-3: the stage's vector-memory work, in this order (vmcnt counts it):
+      // 1. weights of stage s + AH (this tile or the next) into slot kw + AH;
+      // 2. the next chunk's image pieces (first stage of a chunk);
+      // 3. the tile's residuals.  With two operand sets it is issued after the
+      // stage's first MFMA pass, so its scalar work and DMA issue overlap the
+      // other wave's MFMAs instead of holding both waves of a SIMD at the
+      // stage's start
+      auto issue_mem = [&]() {
+        if (!(XDBG & 8)) {
+          if constexpr (s + AH < NST) dma_w(tc.n0, dvc, std::integral_constant<int, (s + AH) % NST>{}, wsa);
+          else dma_w(tx.n0, dvx, std::integral_constant<int, (s + AH) % NST>{}, wsa);
+        }
+        if constexpr (rr == 0) {
+          if constexpr (c + 1 < CH) load_img(tc, std::integral_constant<int, (c + 1 < CH ? c + 1 : 0)>{});
+          else load_img(tx, std::integral_constant<int, 0>{});
+        }
+        if constexpr (s == 0) load_res(tc);
+      };
+      constexpr bool SPLITMF = DBA && !late;
+      if constexpr (!SPLITMF) issue_mem();
       // 4. operands of stage s + 1 into the other register set (the next
       // stage's weights landed and were published one barrier ago)
       const int ws1 = kw + 1 >= NSW ? 0 : kw + 1;
@@ -680,18 +714,27 @@ xconv3_kernel(XP p) {
       // scalar work and reads, and no read is left to the stage's end (where
       // the scheduler would sink them to reuse this stage's registers, and
       // expose their latency).  With one set the reads stay ahead of them
-      if constexpr (!(DBA && !late)) sched_fence();
-      if (!(XDBG & 1)) mfmas(std::integral_constant<int, S>{}, ws1);
+      if constexpr (!SPLITMF) {
+        sched_fence();
+        if (!(XDBG & 1)) mfmas(std::integral_constant<int, S>{}, ws1, std::integral_constant<int, 0>{});
+      } else {
+        // the am pass with the reads interleaved (one or two per MFMA), then
+        // the memory work, then the two ac passes
+        if (!(XDBG & 1)) mfmas(std::integral_constant<int, S>{}, ws1, std::integral_constant<int, 1>{});
 #ifdef __HIP_DEVICE_COMPILE__
-      if constexpr (DBA && !late) {
-        constexpr int NMF = 3 * RW * NT, NRD = 2 * NT + 2 * RW;
-        sfor<(NRD < NMF ? NRD : NMF)>([&](auto) {
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // one MFMA
-          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // one LDS read
+        constexpr int NMA = RW * NT, NRD = 2 * NT + 2 * RW;
+        sfor<NMA>([&](auto k_) {
+          constexpr int k = decltype(k_)::value;
+          constexpr int nr = (k + 1) * NRD / NMA - k * NRD / NMA;
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                          // one MFMA
+          if constexpr (nr > 0) __builtin_amdgcn_sched_group_barrier(0x100, nr, 0);   // LDS reads
         });
-        if constexpr (NMF > NRD) __builtin_amdgcn_sched_group_barrier(0x008, NMF - NRD, 0);
-      }
 #endif
+        sched_fence();
+        issue_mem();
+        sched_fence();
+        if (!(XDBG & 1)) mfmas(std::integral_constant<int, S>{}, ws1, std::integral_constant<int, 2>{});
+      }
       if constexpr (late) {
         if constexpr (DBA) read_a(std::integral_constant<int, 0>{}, ws1);
         read_b(std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{}, ib1);
