@@ -16,7 +16,7 @@ def counter(d, name):
         with open(path) as f:
             for r in csv.DictReader(f):
                 k = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0]
-                if k.startswith("void sconv") or k.startswith("void sgemm"):
+                if k.startswith(("void sconv", "void sgemm", "void xconv")):
                     vals.setdefault(k, []).append(float(r["Counter_Value"]))
     return vals
 

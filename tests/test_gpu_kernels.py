@@ -253,6 +253,37 @@ def test_flow_warp_f32_vector_path_bit_identical():
     assert (got4 - ref).abs().max().item() < 1e-5
 
 
+def test_dwconv3x3_f32_row_blocked_bit_identical():
+    """fp32 4-channel-aligned views take the row-blocked kernel (dw4r_kernel,
+    4 output rows per thread); a view at an even, not 4-aligned channel offset
+    takes the scalar kernel: same taps in the same order, identical bits."""
+    h = K()
+    C, H, W = 128, 19, 37
+    g = torch.Generator().manual_seed(11)
+    big = torch.randn(1, C + 8, H, W, generator=g)
+    w = torch.randn(C, 1, 3, 3, generator=g)
+    b = torch.randn(C, generator=g)
+    w9c = w.reshape(C, 9).t().contiguous().cuda()
+    xa = h.from_nchw(big, h.F32)
+    y4 = h.empty(H, W, C + 8, h.F32)
+    y2 = h.empty(H, W, C + 8, h.F32)
+    h.dwconv3x3(xa.ch(4, C), w9c, b.cuda(), y=y4.ch(4, C))
+    h.dwconv3x3(xa.ch(2, C), w9c, b.cuda(), y=y2.ch(2, C))
+    torch.cuda.synchronize()
+    a4 = back(y4)[:, 4:4 + C]
+    ref = F.conv2d(big[:, 4:4 + C], w, b, padding=1, groups=C)
+    assert rel_err(a4, ref) < 1e-5
+    ref2 = F.conv2d(big[:, 2:2 + C], w, b, padding=1, groups=C)
+    a2 = back(y2)[:, 2:2 + C]
+    assert rel_err(a2, ref2) < 1e-5
+    # same input channels through both kernels: shift the scalar path's view
+    y3 = h.empty(H, W, C + 8, h.F32)
+    big2 = torch.cat([big[:, 2:], big[:, :2]], dim=1)   # channel 4 + k of big at 2 + k
+    h.dwconv3x3(h.from_nchw(big2, h.F32).ch(2, C), w9c, b.cuda(), y=y3.ch(2, C))
+    torch.cuda.synchronize()
+    assert torch.equal(a4, back(y3)[:, 2:2 + C])
+
+
 def test_resize_and_pool():
     from oracle.dc_oracle import up2, down2
     h = K()
