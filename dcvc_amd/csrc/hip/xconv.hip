@@ -117,9 +117,28 @@ struct XG {
   // their DMA was issued by stage s + 2 - AH (of this tile or the previous
   // one, the schedule repeats per tile); the operations issued after it may
   // stay in flight (vmcnt counts them in issue order)
-  static constexpr int wait_for(int s, int ah) {
+  static constexpr int wait_for_old(int s, int ah) {
     int n = after_dma((s + 2 - ah + 2 * NST) % NST);
     for (int k = 1; k < ah - 1; ++k) n += all_ops((s + 2 - ah + k + 2 * NST) % NST);
+    return n;
+  }
+  // Barriers at every other stage (PB): at the end of odd stages and of the
+  // tile's last stage.  A barrier stage s then waits for the weights read
+  // before the next barrier: the reads of stages s + 1 .. nb (the next
+  // barrier stage) take stages s + 2 .. nb + 1, so DMA(nb + 1) must have
+  // landed; non-barrier stages wait for nothing
+  static constexpr bool PB = true;
+  static constexpr bool bar(int s) { return !PB || (s % 2 == 1) || s == NST - 1; }
+  static constexpr int next_bar(int s) {   // extended stage index (past NST: the next tile)
+    for (int x = s + 1; x < s + 2 * NST + 2; ++x)
+      if (bar(x % NST)) return x;
+    return s + 1;
+  }
+  static constexpr int wait_for(int s, int ah) {
+    if (!bar(s)) return 63;   // (unused)
+    const int x0 = next_bar(s) + 1 - ah;   // the stage that issued DMA(nb + 1), <= s
+    int n = after_dma((x0 + 2 * NST) % NST);
+    for (int x = x0 + 1; x <= s; ++x) n += all_ops((x + 2 * NST) % NST);
     return n;
   }
   // weight ring: NSW slots, the DMA of a stage issued AH = NSW - 1 stages
@@ -142,7 +161,8 @@ struct XG {
     if (n > NST + 1) n = NST + 1;
     for (; n > 4; --n) {
       int worst = 0;
-      for (int x = 0; x < NST; ++x) worst = wait_for(x, n - 1) > worst ? wait_for(x, n - 1) : worst;
+      for (int x = 0; x < NST; ++x)
+        if (bar(x)) worst = wait_for(x, n - 1) > worst ? wait_for(x, n - 1) : worst;
       if (worst < 64) break;
     }
     return n;
@@ -746,13 +766,17 @@ xconv3_kernel(XP p) {
       {
         constexpr int cn = c + 1 < CH ? c + 1 : 0;
         constexpr int PPn = cn == CH - 1 ? PPL : PPF;
-        constexpr int w0 = rows - 1 - PPn;   // the first publishing stage
+        // (the last piece at a stage that ends with a barrier before the
+        // chunk's last stage)
+        constexpr int s0c = s - rr;   // the chunk's first stage
+        constexpr int pend = G::bar(s0c + rows - 2) ? rows - 2 : rows - 3;
+        constexpr int w0 = pend + 1 - PPn;   // the first publishing stage
         using CN = std::integral_constant<int, cn>;
         if constexpr (w0 >= 1) {
-          if constexpr (rr >= w0 && rr <= rows - 2)
+          if constexpr (rr >= w0 && rr <= pend)
             if (!(XDBG & 16))
               publish(q ^ 1, CN{}, std::integral_constant<int, rr - w0>{}, std::integral_constant<int, rr - w0 + 1>{});
-        } else if constexpr (rr == rows - 2) {
+        } else if constexpr (rr == pend) {
           if (!(XDBG & 16)) publish(q ^ 1, CN{}, std::integral_constant<int, 0>{}, std::integral_constant<int, PPn>{});
         }
       }
@@ -767,7 +791,7 @@ xconv3_kernel(XP p) {
       if (2 * s + 1 < 64 && t == g + G0)
         asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(stampv) : "s"((unsigned)__builtin_amdgcn_s_memtime()), "i"(2 * s));
 #endif
-      {
+      if constexpr (G::bar(s)) {
         constexpr int N = G::wait_n(s);
         static_assert(N < 64, "too many vector-memory operations in flight for vmcnt");
         if (XDBG & 4) wait_lgkm();
@@ -777,7 +801,8 @@ xconv3_kernel(XP p) {
       // stay between its operand reads and its barrier, so operand and
       // accumulator registers live one stage long
       sched_fence();
-      if (!(XDBG & 2)) raw_barrier();
+      if constexpr (G::bar(s))
+        if (!(XDBG & 2)) raw_barrier();
       sched_fence();
 #ifdef XCONV_DBG
       if (2 * s + 1 < 64 && t == g + G0)
