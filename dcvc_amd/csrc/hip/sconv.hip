@@ -647,7 +647,12 @@ int g_res_waves = 0;
 template <int KS, int S, bool GATE>
 int pick_bn(SP p, hipStream_t st) {
   int order[4];
-  if constexpr (KS != 7) {
+  // stride-2 3x3 layers stream their weights: a 32- or 16-channel resident
+  // n-block re-reads the 4x larger input once per n-block, and the streamed
+  // 48/64-channel blocks win at every DC shape (128->96 at 544x960 436 -> 267
+  // us, 64->64 at 1088x1920 367 -> 320, 48->64 303 -> 280, 56->64 346 vs 348;
+  // scripts/gpu_r04o.sh, profiles/r04o_sconv_s2_ab.jsonl)
+  if constexpr (KS != 7 && !(KS == 3 && S == 2)) {
     // resident weights where they fit
     if (g_resident) {
       bn_order(p.cout, 64, order);
