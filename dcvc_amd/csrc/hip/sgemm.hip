@@ -407,15 +407,18 @@ extern "C" int dcvc_internal_sgemm(const dcvc_conv_args *a, void *stream) {
   }
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (g_cfg > 0) return run_cfg(g_cfg, p, st);
-  // auto: n-blocks by padded output channels (fewest first, wider first);
-  // 2 pixel groups per wave while that still gives a workgroup per CU, else 1
+  // auto: n-blocks by padded output channels (fewest first; 64 before 128 on
+  // a tie); 2 pixel groups per wave while that still gives 8 workgroups per
+  // CU, else 1.  scripts/gpu_r04q.sh (profiles/r04q_sgemm_ab.jsonl): 128 ->
+  // 128 at 272x480 49.1 -> 37.0 us, 384 -> 384 at 68x120 18.4 -> 16.3 us, the
+  // 1080p 1x1 layers unchanged (BN 128 never ahead)
   if (g_cus <= 0) {
     int dev = 0;
     hipDeviceProp_t prop;
     if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess) return DCVC_HIP_ELAUNCH;
     g_cus = prop.multiProcessorCount;
   }
-  int order[3] = {128, 64, 32};
+  int order[3] = {64, 128, 32};
   auto padded = [&](int bn) { return (p.cout + bn - 1) / bn * bn - p.cout; };
   for (int i = 0; i < 3; ++i)
     for (int j = i + 1; j < 3; ++j)
@@ -426,7 +429,7 @@ extern "C" int dcvc_internal_sgemm(const dcvc_conv_args *a, void *stream) {
       const int bn = order[i];
       if (padded(bn) > padded(order[0])) break;
       const int64_t nt = (np + 64 * pxw - 1) / (64 * pxw) * ((p.cout + bn - 1) / bn);
-      if (nt >= g_cus) return run_cfg(cfg_of(bn, pxw), p, st);
+      if (nt >= (pxw == 2 ? 8 : 1) * g_cus) return run_cfg(cfg_of(bn, pxw), p, st);
     }
   return run_cfg(cfg_of(order[0], 1), p, st);
 }
