@@ -41,9 +41,12 @@ STRICT_PRECISIONS = ("split", "parity")
 
 # the strict teacher-forced GPU test that holds each workload's arithmetic to
 # the bar at full size (tests/test_gpu_parity_strict.py), by (model, yuv420)
-STRICT_TESTS = {("dc", False): "tests/test_gpu_parity_strict.py::test_strict_parity_c3_1080p",
-                ("hem", False): "tests/test_gpu_parity_strict.py::test_strict_parity_hem_c2_1080p",
-                ("dc", True): "tests/test_gpu_parity_strict.py::test_strict_parity_c4_yuv420"}
+STRICT_TESTS = {("dc", False): ("tests/test_gpu_parity_strict.py::test_strict_parity_c3_1080p",
+                                 "I + P frames at 1920x1080"),
+                ("hem", False): ("tests/test_gpu_parity_strict.py::test_strict_parity_hem_c2_1080p",
+                                 "I + P frames at 1920x1080"),
+                ("dc", True): ("tests/test_gpu_parity_strict.py::test_strict_parity_c4_yuv420",
+                               "I-frame at 3840x2160, I + P frames at 1920x1080")}
 
 
 def parity_evidence(args, parity):
@@ -55,7 +58,8 @@ def parity_evidence(args, parity):
     if parity is not None:
         return "parity_check passed" if parity.get("passed") else "parity_check FAILED"
     t = STRICT_TESTS.get((args.model, bool(args.yuv420)))
-    return f"strict GPU test {t} ({args.precision} precision)" if t else "unpinned"
+    return (f"strict GPU test {t[0]} ({args.precision} precision; {t[1]}), not this run's frames" if t
+            else "unpinned")
 
 
 def metric_name(args, parity=None):
@@ -70,6 +74,10 @@ def metric_name(args, parity=None):
         return f"{base}; parity check FAILED against the oracle (see parity_check)"
     if ev == "unpinned":
         return f"{base}; parity unpinned"
+    if parity is None:
+        # no check of this run's frames: say which test holds the arithmetic
+        t = STRICT_TESTS[(args.model, bool(args.yuv420))]
+        return f"{base}; bpp bit-exact + PSNR \u0394<1e-4 dB vs ref (strict GPU test, {t[1]}; not this run's frames)"
     return f"{base}; bpp bit-exact + PSNR \u0394<1e-4 dB vs ref"
 
 
@@ -307,6 +315,7 @@ def _workers_record(args):
     # the record's rate per worker core and, for scale, that rate times this
     # node's physical cores (linear scaling assumed: an upper bound, the
     # workers share memory bandwidth)
+    rec["source"] = "profiles/cpu_baseline_workers.json (committed record, not re-measured in this run)"
     rec["per_core_fps"] = rec["value"] / rec["cores"]
     pc = host_info()["physical_cores"]
     if pc:
@@ -440,6 +449,78 @@ def launch_ranks(args):
     return subprocess.call(cmd, env=env)
 
 
+def parse_cpulist(text):
+    """'0-3,8,10-11' -> [0, 1, 2, 3, 8, 10, 11]."""
+    out = []
+    for part in text.strip().split(","):
+        if not part:
+            continue
+        a, _, b = part.partition("-")
+        out.extend(range(int(a), int(b or a) + 1))
+    return out
+
+
+def gpu_cpulists(n):
+    """The host CPUs local to each of the first n visible GPUs (their PCI
+    device's NUMA node, from sysfs), or None where sysfs does not say."""
+    out = []
+    for i in range(n):
+        try:
+            p = torch.cuda.get_device_properties(i)
+            bus = f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}.0"
+            with open(f"/sys/bus/pci/devices/{bus}/local_cpulist") as f:
+                out.append(parse_cpulist(f.read()))
+        except (OSError, AttributeError, ValueError, RuntimeError):
+            out.append(None)
+    return out
+
+
+def rank_cpu_plan(local, local_world, lists, allowed):
+    """The host cores of local rank `local` (one process per GPU, local_world
+    of them on this node): the cores local to its GPU that this process may
+    use, split evenly between the ranks whose GPUs share that NUMA node, so
+    no two ranks' coder threads and GOP lanes run on one core.  `lists`:
+    gpu_cpulists(local_world); `allowed`: the process's affinity.  Falls back
+    to an even split of `allowed` when sysfs gives no NUMA placement."""
+    allowed = sorted(allowed)
+    mine = lists[local] if local < len(lists) else None
+    if mine:
+        pool = [c for c in mine if c in set(allowed)]
+        peers = [r for r in range(local_world) if r < len(lists) and lists[r] and set(lists[r]) == set(mine)]
+    else:
+        pool, peers = allowed, list(range(local_world))
+    if not pool:
+        pool, peers = allowed, list(range(local_world))
+    k = peers.index(local) if local in peers else 0
+    n = len(peers) or 1
+    per = max(1, len(pool) // n)
+    share = pool[k * per:(k + 1) * per] if len(pool) >= n else pool
+    return share or allowed
+
+
+def pin_rank(local, local_world, lanes, parts):
+    """Pin this rank to its share of the host (rank_cpu_plan) and size the
+    rANS worker pool to it: parts - 1 workers at most (a frame's stream parts
+    are coded by the workers plus the lane's own thread), at most the share
+    less the lanes' threads.  Returns the plan for the bench line."""
+    from dcvc_amd._native import rans_lib
+    try:
+        allowed = sorted(os.sched_getaffinity(0))
+    except AttributeError:
+        allowed = list(range(os.cpu_count() or 1))
+    lists = gpu_cpulists(local_world)
+    share = rank_cpu_plan(local, local_world, lists, allowed)
+    try:
+        os.sched_setaffinity(0, share)
+    except (AttributeError, OSError):
+        pass
+    workers = max(1, min(parts - 1, len(share) - lanes))
+    rc = rans_lib().dcvc_rans_set_threads(workers)
+    return {"cores": len(share), "cpus": f"{share[0]}-{share[-1]}" if share else "",
+            "numa_local": lists[local] is not None if local < len(lists) else False,
+            "coder_workers": workers if rc == 0 else rans_lib().dcvc_rans_threads(), "lane_threads": lanes}
+
+
 def launcher_selftest(args):
     """--launcher-selftest: the rank plumbing of the N-GPU bench without a GPU
     (gloo): every rank joins, contributes its rank, and rank 0 prints one JSON
@@ -451,9 +532,27 @@ def launcher_selftest(args):
     dist.all_reduce(t)
     dist.barrier()
     elapsed = max_over_ranks(dist, 0.001 * (rank + 1), "cpu")
+    # the host plan each rank would take on a node whose GPUs sit on two NUMA
+    # nodes of the allowed cores (sysfs is not read here: no GPU)
+    local = int(os.environ.get("LOCAL_RANK", rank))
+    allowed = sorted(os.sched_getaffinity(0))
+    half = len(allowed) // 2
+    lists = [allowed[:half] if r < world // 2 else allowed[half:] for r in range(world)]
+    share = rank_cpu_plan(local, world, lists, allowed)
+    from dcvc_amd._native import rans_lib
+    L = rans_lib()
+    workers = max(1, min(args.stream_part - 1, len(share) - args.lanes))
+    set_rc = L.dcvc_rans_set_threads(workers)
+    from dcvc_amd import rans as P
+    coders = [(P.RansEncoder(True, args.stream_part), P.RansDecoder(args.stream_part))
+              for _ in range(2 * args.lanes)]
+    nthreads = len(os.listdir("/proc/self/task"))
+    plans = [None] * world
+    dist.all_gather_object(plans, {"rank": rank, "share": share, "coder_workers": L.dcvc_rans_threads(),
+                                   "set_rc": set_rc, "coders": len(coders), "threads": nthreads})
     if rank == 0:
         print(json.dumps({"n_gpus": world, "ranks_joined": int(t[0]), "rank_sum": int(t[1]),
-                          "max_elapsed": elapsed, "requested": args.gpus}), flush=True)
+                          "max_elapsed": elapsed, "requested": args.gpus, "plans": plans}), flush=True)
     dist.destroy_process_group()
 
 
@@ -617,6 +716,7 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
+    host_plan = pin_rank(local, int(os.environ.get("LOCAL_WORLD_SIZE", world)), args.lanes, args.stream_part)
 
     from dcvc_amd import hip as K
     from dcvc_amd.layers import Precision
@@ -871,6 +971,7 @@ def main():
                       "fast": "bf16 features, fp32 entropy params",
                       "fast-bf16-tail": "bf16 (entropy-parameter tail in bf16 too)"}[args.precision],
             "data": "synthetic (moving sinusoid + noise frames, seeded random weights)",
+            "host_plan": host_plan,
             "config": {"workload": (f"C2 DCVC-HEM RGB {w}x{h} (zero pad {W}x{H}) IP={args.gop} write mode"
                                     if hem else
                                     f"C4 DCVC-DC YUV420 {w}x{h} (pad {W}x{H}) IP={args.gop} write mode" if args.yuv420

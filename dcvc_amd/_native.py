@@ -75,6 +75,8 @@ RANS_SYMBOLS = [
      [_vp, _i16p, _c.c_int64, _i32p, _c.c_int, _c.c_int, _i32p, _i32p, _i16p]),
     ("dcvc_rans_dec_decode_table_i16", _c.c_int, [_vp, _i16p, _c.c_int64, _vp, _i16p]),
     ("dcvc_rans_dec_decode_table_i32", _c.c_int, [_vp, _i32p, _c.c_int64, _vp, _i32p]),
+    ("dcvc_rans_set_threads", _c.c_int, [_c.c_int]),
+    ("dcvc_rans_threads", _c.c_int, []),
 ]
 
 

@@ -301,6 +301,159 @@ __global__ void __launch_bounds__(256) offset_div_kernel(View feat, View offs, V
   }
 }
 
+// ---- OffsetDiversity on fp32 maps (Precision.split / parity), group-planar.
+//
+// The kernel above runs one thread per (pixel, group) with a wave holding 4
+// pixels x 16 groups: every group samples at its own offset, so each of its
+// eight 12-byte corner gathers touches 64 different cache lines, and the L1
+// tag lookups, not bytes, bound it.  Here the 48-channel
+// feature is first copied group-planar, P[16][H][W][3] (planar3_kernel), and a
+// wave holds 64 neighbouring pixels of ONE group: their corners lie in a few
+// consecutive 12-byte cells of one plane (6-7 lines per gather instead of 64).
+// The half-resolution offset rows a block needs are staged in LDS with
+// coalesced 16-byte loads, and the 48 output channels of the block's pixels
+// are staged in LDS and stored as whole pixels.  Per element the arithmetic
+// is offset_div_kernel's, in the same order: identical results.
+constexpr int OD_PX = 64;    // pixels of one row per workgroup
+constexpr int OD_OCOLS = 34; // half-resolution offset columns such a run reads
+constexpr int OD_OST = 100;  // LDS floats per staged offset pixel (96 + pad)
+
+// NHWC 48-channel fp32 -> P[16][H][W][3], one workgroup per 64 pixels (flat
+// pixel order), through LDS: coalesced 16-byte loads and stores
+__global__ void __launch_bounds__(256) planar3_kernel(View x, float *P, int64_t npix) {
+  __shared__ float s[OD_PX * 49];
+  const int64_t pix0 = (int64_t)blockIdx.x * OD_PX;
+  const int n = (int)(npix - pix0 < OD_PX ? npix - pix0 : OD_PX);
+  const float *xp = reinterpret_cast<const float *>(x.p) + x.co;
+  for (int i = threadIdx.x; i < n * 12; i += 256) {
+    const int p = i / 12, q = i - p * 12;
+    const float4 v = *reinterpret_cast<const float4 *>(xp + (pix0 + p) * x.cs + 4 * q);
+    float *d = s + p * 49 + 4 * q;
+    d[0] = v.x, d[1] = v.y, d[2] = v.z, d[3] = v.w;
+  }
+  __syncthreads();
+  if (n == OD_PX) {
+    // group sg: 192 contiguous floats = 48 float4 (pix0 * 3 floats is 16-byte aligned)
+    for (int i = threadIdx.x; i < 16 * 48; i += 256) {
+      const int sg = i / 48, q = i - sg * 48;
+      float4 v;
+      float *e = &v.x;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int f = 4 * q + k, p = f / 3, c = f - p * 3;
+        e[k] = s[p * 49 + 3 * sg + c];
+      }
+      *reinterpret_cast<float4 *>(P + (int64_t)sg * npix * 3 + pix0 * 3 + 4 * q) = v;
+    }
+  } else {
+    for (int i = threadIdx.x; i < 16 * n * 3; i += 256) {
+      const int sg = i / (n * 3), f = i - sg * n * 3, p = f / 3, c = f - p * 3;
+      P[(int64_t)sg * npix * 3 + pix0 * 3 + f] = s[p * 49 + 3 * sg + c];
+    }
+  }
+}
+
+__global__ void __launch_bounds__(256) offset_div_pl_kernel(const float *P, View offs, View flow, View y,
+                                                            const float *fw, const float *fb, const float *gx,
+                                                            const float *gy, float mag) {
+  __shared__ float sfw[48 * 6], sfb[48];
+  __shared__ __align__(16) float so[2 * OD_OCOLS * OD_OST];   // offset rows h0, h1
+  __shared__ float sy[OD_PX * 49];                            // output pixels
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int py = blockIdx.y, px0 = blockIdx.x * OD_PX;
+  const int W = y.W, H = y.H;
+  for (int i = tid; i < 48 * 6; i += 256) sfw[i] = fw[i];
+  if (tid < 48) sfb[tid] = fb[tid];
+  // the two half-resolution rows and the columns [c0, c0 + OD_OCOLS) of the
+  // offset map this row of pixels interpolates from (up2_at's geometry)
+  float syf = 0.5f * ((float)py + 0.5f) - 0.5f;
+  syf = syf < 0.f ? 0.f : syf;
+  const int h0 = (int)syf, h1 = h0 + (h0 < offs.H - 1 ? 1 : 0);
+  const float hl1 = syf - (float)h0, hl0 = 1.f - hl1;
+  const int c0 = px0 / 2 > 0 ? px0 / 2 - 1 : 0;
+  const int nc = offs.W - c0 < OD_OCOLS ? offs.W - c0 : OD_OCOLS;
+  const float *op = reinterpret_cast<const float *>(offs.p) + offs.co;
+  for (int i = tid; i < 2 * nc * 24; i += 256) {
+    const int r = i / (nc * 24), f = i - r * nc * 24, c = f / 24, q = f - c * 24;
+    const float4 v = *reinterpret_cast<const float4 *>(op + ((int64_t)(r ? h1 : h0) * offs.W + c0 + c) * offs.cs + 4 * q);
+    *reinterpret_cast<float4 *>(so + (r * OD_OCOLS + c) * OD_OST + 4 * q) = v;
+  }
+  __syncthreads();
+  const int px = px0 + lane;
+  const bool live = px < W;
+  const int pxc = live ? px : W - 1;
+  const int64_t pix = (int64_t)py * W + pxc;
+  const float2 fv = *reinterpret_cast<const float2 *>(reinterpret_cast<const float *>(flow.p) + pix * flow.cs + flow.co);
+  float sxf = 0.5f * ((float)pxc + 0.5f) - 0.5f;
+  sxf = sxf < 0.f ? 0.f : sxf;
+  const int w0 = (int)sxf, w1 = w0 + (w0 < offs.W - 1 ? 1 : 0);
+  const float wl1 = sxf - (float)w0, wl0 = 1.f - wl1;
+  const float *o00 = so + (w0 - c0) * OD_OST, *o01 = so + (w1 - c0) * OD_OST;
+  const float *o10 = so + (OD_OCOLS + w0 - c0) * OD_OST, *o11 = so + (OD_OCOLS + w1 - c0) * OD_OST;
+  const float gxv = gx[pxc], gyv = gy[py];
+  const int64_t plane = (int64_t)H * W * 3;
+  // wave w: groups w, w + 4, w + 8, w + 12
+#pragma unroll 1
+  for (int gi = 0; gi < 4; ++gi) {
+    const int g = wave + 4 * gi;
+    float ov[6];
+    {
+      float cv[4][6];
+      const float *cs4[4] = {o00, o01, o10, o11};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float4 a = *reinterpret_cast<const float4 *>(cs4[k] + 4 * g);
+        const float2 m = *reinterpret_cast<const float2 *>(cs4[k] + 64 + 2 * g);
+        cv[k][0] = a.x, cv[k][1] = a.y, cv[k][2] = a.z, cv[k][3] = a.w, cv[k][4] = m.x, cv[k][5] = m.y;
+      }
+#pragma unroll
+      for (int j = 0; j < 6; ++j) ov[j] = (cv[0][j] * wl0 + cv[1][j] * wl1) * hl0 + (cv[2][j] * wl0 + cv[3][j] * wl1) * hl1;
+    }
+    float xm[6];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int i = 2 * g + k;
+      float dx = mag * tanhf(ov[2 * k]);
+      float dy = mag * tanhf(ov[2 * k + 1]);
+      dx = dx + fv.x;
+      dy = dy + fv.y;
+      const float msk = sigmoidf_(ov[4 + k]);
+      const Bilin b = warp_coords(gxv, gyv, dx, dy, W, H);
+      const float *base = P + (i & 15) * plane;
+      const int r0 = b.y0 * W, r1 = b.y1 * W;
+      const int e[4] = {(r0 + b.x0) * 3, (r0 + b.x1) * 3, (r1 + b.x0) * 3, (r1 + b.x1) * 3};
+      float q[4][3];
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) {
+        const f32x3a4 wv = *reinterpret_cast<const f32x3a4 *>(base + e[kk]);
+        q[kk][0] = wv.a;
+        q[kk][1] = wv.b;
+        q[kk][2] = wv.c;
+      }
+#pragma unroll
+      for (int c = 0; c < 3; ++c)
+        xm[3 * k + c] = (q[0][c] * b.nw + q[1][c] * b.ne + q[2][c] * b.sw + q[3][c] * b.se) * msk;
+    }
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      const int o = 3 * g + c;
+      float acc = 0.f;
+#pragma unroll
+      for (int k = 0; k < 6; ++k) acc = acc + sfw[o * 6 + k] * xm[k];
+      sy[lane * 49 + o] = acc + sfb[o];
+    }
+  }
+  __syncthreads();
+  // whole output pixels: 12 float4 each
+  const int n = W - px0 < OD_PX ? W - px0 : OD_PX;
+  float *yp = reinterpret_cast<float *>(y.p) + y.co;
+  for (int i = tid; i < n * 12; i += 256) {
+    const int p = i / 12, q = i - p * 12;
+    const float *s = sy + p * 49 + 4 * q;
+    *reinterpret_cast<float4 *>(yp + ((int64_t)py * W + px0 + p) * y.cs + 4 * q) = make_float4(s[0], s[1], s[2], s[3]);
+  }
+}
+
 template <typename TX, typename TY>
 __global__ void resize_kernel(View x, View y, int up, float mul) {
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -437,6 +590,37 @@ extern "C" int dcvc_offset_diversity(dcvc_tensor feat, dcvc_tensor offs, dcvc_te
     else LAUNCH(uint16_t, float, uint16_t, false);
   } else return DCVC_HIP_EUNSUPPORTED;
 #undef LAUNCH
+  DCVC_LAUNCH_CHECK();
+  return DCVC_HIP_OK;
+}
+
+extern "C" int64_t dcvc_offset_diversity_workspace(int H, int W) {
+  return H > 0 && W > 0 ? (int64_t)16 * H * W * 3 * 4 : 0;
+}
+
+extern "C" int dcvc_offset_diversity_ws(dcvc_tensor feat, dcvc_tensor offs, dcvc_tensor flow, dcvc_tensor y,
+                                        const float *fw, const float *fb, const float *gx, const float *gy,
+                                        float max_mag, void *workspace, int64_t ws_bytes, void *stream) {
+  if (!ok(feat) || !ok(offs) || !ok(flow) || !ok(y) || !fw || !fb || !gx || !gy) return DCVC_HIP_EINVAL;
+  if (feat.C != 48 || y.C != 48 || offs.C != 96 || flow.C != 2 || flow.dtype != DCVC_F32 || feat.H != y.H ||
+      feat.W != y.W || flow.H != y.H || flow.W != y.W || offs.H * 2 != y.H || offs.W * 2 != y.W)
+    return DCVC_HIP_EINVAL;
+  const bool vec = feat.dtype == DCVC_F32 && offs.dtype == DCVC_F32 && y.dtype == DCVC_F32 &&
+                   feat.cstride % 4 == 0 && feat.coff % 4 == 0 && ((uintptr_t)feat.ptr & 15) == 0 &&
+                   offs.cstride % 4 == 0 && offs.coff % 4 == 0 && ((uintptr_t)offs.ptr & 15) == 0 &&
+                   y.cstride % 4 == 0 && y.coff % 4 == 0 && ((uintptr_t)y.ptr & 15) == 0 &&
+                   flow.cstride % 2 == 0 && flow.coff % 2 == 0 && ((uintptr_t)flow.ptr & 7) == 0 &&
+                   (int64_t)y.H * y.W * 3 < ((int64_t)1 << 31);
+  // (no workspace or another layout: the pixel-major kernel)
+  if (!vec || !workspace || ((uintptr_t)workspace & 15) || ws_bytes < dcvc_offset_diversity_workspace(y.H, y.W))
+    return dcvc_offset_diversity(feat, offs, flow, y, fw, fb, gx, gy, max_mag, stream);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int64_t npix = (int64_t)y.H * y.W;
+  float *P = reinterpret_cast<float *>(workspace);
+  hipLaunchKernelGGL(planar3_kernel, dim3((unsigned)((npix + OD_PX - 1) / OD_PX)), dim3(256), 0, st, mk(feat), P, npix);
+  DCVC_LAUNCH_CHECK();
+  hipLaunchKernelGGL(offset_div_pl_kernel, dim3((unsigned)((y.W + OD_PX - 1) / OD_PX), (unsigned)y.H), dim3(256), 0,
+                     st, P, mk(offs), mk(flow), mk(y), fw, fb, gx, gy, max_mag);
   DCVC_LAUNCH_CHECK();
   return DCVC_HIP_OK;
 }

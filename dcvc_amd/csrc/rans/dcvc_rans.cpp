@@ -21,6 +21,7 @@
 #include "../../../include/dcvc_rans.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <atomic>
 #include <cmath>
 #include <condition_variable>
@@ -123,13 +124,73 @@ struct CdfTable {
 };
 
 // ---------------------------------------------------------------- pool
-// Runs fn(0..tasks-1) on the calling thread plus `workers` persistent threads
-// and returns when every task is done.  Task indices are claimed with a CAS
-// on (generation << 32 | next), so a worker that wakes late can never run a
-// task of a later batch with an earlier batch's function.
+// One process-wide pool of persistent worker threads shared by every encoder
+// and decoder (several GOP lanes, each with an I- and a P-codec, would
+// otherwise each keep stream_part - 1 threads: 84 per process at 3 lanes x 4
+// coder objects x 7).  run(tasks, fn) queues a batch, works on it on the
+// calling thread too, and returns when all of its tasks are done; batches of
+// concurrent callers are served in arrival order.  Workers default to
+// min(15, hardware threads - 1), set by dcvc_rans_set_threads (or the
+// DCVC_CODER_THREADS environment variable) before the first coder call.
 class Pool {
  public:
+  static Pool &shared() {
+    static Pool p(configured());
+    return p;
+  }
+  static int configured() {
+    int n = g_threads.load();
+    if (n < 0) {
+      const char *e = std::getenv("DCVC_CODER_THREADS");
+      n = e ? std::atoi(e) : -1;
+    }
+    if (n < 0) {
+      const int hw = (int)std::thread::hardware_concurrency();
+      n = std::min(15, std::max(0, hw - 1));
+    }
+    return std::min(n, 64);
+  }
+  static std::atomic<int> g_threads;
+  static std::atomic<bool> g_started;
+  int workers() const { return (int)th_.size(); }
+
+  void run(int tasks, const std::function<void(int)> &fn) {
+    if (tasks <= 0) return;
+    if (th_.empty() || tasks == 1) {
+      for (int i = 0; i < tasks; ++i) fn(i);
+      return;
+    }
+    Batch b;
+    b.fn = &fn;
+    b.tasks = tasks;
+    b.remaining = tasks;
+    std::unique_lock<std::mutex> lk(mu_);
+    q_.push_back(&b);
+    lk.unlock();
+    cv_.notify_all();
+    int i;
+    for (;;) {
+      lk.lock();
+      const bool got = claim(&b, &i);
+      lk.unlock();
+      if (!got) break;
+      fn(i);
+      lk.lock();
+      --b.remaining;
+      lk.unlock();
+    }
+    lk.lock();
+    b.done.wait(lk, [&b] { return b.remaining == 0; });
+  }
+
+ private:
+  struct Batch {
+    const std::function<void(int)> *fn = nullptr;
+    int tasks = 0, next = 0, remaining = 0;
+    std::condition_variable done;
+  };
   explicit Pool(int workers) {
+    g_started = true;
     for (int i = 0; i < workers; ++i) th_.emplace_back([this] { loop(); });
   }
   ~Pool() {
@@ -140,78 +201,38 @@ class Pool {
     cv_.notify_all();
     for (auto &t : th_) t.join();
   }
-  void run(int tasks, const std::function<void(int)> &fn) {
-    if (tasks <= 0) return;
-    if (th_.empty() || tasks == 1) {
-      for (int i = 0; i < tasks; ++i) fn(i);
-      return;
+  // under mu_: the next task of b; a batch with none left leaves the queue
+  // (so no worker can reach it after its caller has returned)
+  bool claim(Batch *b, int *idx) {
+    if (b->next < b->tasks) {
+      *idx = b->next++;
+      if (b->next == b->tasks) q_.erase(std::remove(q_.begin(), q_.end(), b), q_.end());
+      return true;
     }
-    uint32_t gen;
-    {
-      std::lock_guard<std::mutex> lk(mu_);
-      gen = ++gen_;
-      fn_ = &fn;
-      tasks_ = tasks;
-      remaining_ = tasks;
-      next_.store((uint64_t)gen << 32, std::memory_order_release);
-    }
-    cv_.notify_all();
-    work(gen, fn, tasks);
-    std::unique_lock<std::mutex> lk(mu_);
-    done_.wait(lk, [this] { return remaining_ == 0; });
-    fn_ = nullptr;
-  }
-
- private:
-  bool claim(uint32_t gen, int tasks, int *idx) {
-    uint64_t v = next_.load(std::memory_order_acquire);
-    for (;;) {
-      if ((uint32_t)(v >> 32) != gen || (int)(uint32_t)v >= tasks) return false;
-      if (next_.compare_exchange_weak(v, v + 1, std::memory_order_acq_rel)) {
-        *idx = (int)(uint32_t)v;
-        return true;
-      }
-    }
-  }
-  void work(uint32_t gen, const std::function<void(int)> &fn, int tasks) {
-    int i, n = 0;
-    while (claim(gen, tasks, &i)) {
-      fn(i);
-      ++n;
-    }
-    if (n) {
-      std::lock_guard<std::mutex> lk(mu_);
-      remaining_ -= n;
-      if (remaining_ == 0) done_.notify_all();
-    }
+    return false;
   }
   void loop() {
-    uint32_t seen = 0;
+    std::unique_lock<std::mutex> lk(mu_);
     for (;;) {
-      const std::function<void(int)> *fn;
-      uint32_t gen;
-      int tasks;
-      {
-        std::unique_lock<std::mutex> lk(mu_);
-        cv_.wait(lk, [&] { return stop_ || (gen_ != seen && fn_ != nullptr); });
-        if (stop_) return;
-        seen = gen = gen_;
-        fn = fn_;
-        tasks = tasks_;
-      }
-      work(gen, *fn, tasks);
+      cv_.wait(lk, [this] { return stop_ || !q_.empty(); });
+      if (stop_) return;
+      Batch *b = q_.front();
+      int i;
+      if (!claim(b, &i)) continue;
+      lk.unlock();
+      (*b->fn)(i);
+      lk.lock();
+      if (--b->remaining == 0) b->done.notify_all();
     }
   }
   std::vector<std::thread> th_;
   std::mutex mu_;
-  std::condition_variable cv_, done_;
-  std::atomic<uint64_t> next_{0};
-  const std::function<void(int)> *fn_ = nullptr;
-  uint32_t gen_ = 0;
-  int tasks_ = 0;
-  int remaining_ = 0;
+  std::condition_variable cv_;
+  std::vector<Batch *> q_;
   bool stop_ = false;
 };
+std::atomic<int> Pool::g_threads{-1};
+std::atomic<bool> Pool::g_started{false};
 
 // ---------------------------------------------------------------- encoder
 struct Record {                      // one encode call's slice of a part
@@ -334,7 +355,7 @@ struct dcvc_cdf_table {
 struct dcvc_rans_enc {
   int parts = 1;
   std::vector<EncPart> part;
-  std::unique_ptr<Pool> pool;
+  Pool *pool = nullptr;
   int status = DCVC_OK;   // first failure of an encode call since reset
 };
 
@@ -343,7 +364,7 @@ struct dcvc_rans_dec {
   std::vector<std::vector<uint32_t>> words;  // per part
   std::vector<size_t> pos;                   // next word to read
   std::vector<uint64_t> state;
-  std::unique_ptr<Pool> pool;
+  Pool *pool = nullptr;
 };
 
 namespace {
@@ -560,10 +581,10 @@ dcvc_rans_enc *dcvc_rans_enc_create(int multithread, int stream_part) {
   e->parts = stream_part;
   e->part.resize(stream_part);
   // reference: multiThread || streamPart > 1 selects the threaded encoder
-  // (py_rans.cpp:11-20); here the parts are worked on by a pool of
-  // stream_part - 1 threads plus the caller.  The stream is the same either way.
+  // (py_rans.cpp:11-20); here the parts are worked on by the process-wide
+  // pool plus the caller.  The stream is the same either way.
   (void)multithread;
-  e->pool.reset(new Pool(stream_part - 1));
+  e->pool = &Pool::shared();
   return e;
 }
 
@@ -679,7 +700,7 @@ dcvc_rans_dec *dcvc_rans_dec_create(int stream_part) {
   auto *d = new (std::nothrow) dcvc_rans_dec;
   if (!d) return nullptr;
   d->parts = stream_part;
-  d->pool.reset(new Pool(stream_part - 1));
+  d->pool = &Pool::shared();
   return d;
 }
 
@@ -746,3 +767,12 @@ int dcvc_rans_dec_decode_table_i32(dcvc_rans_dec *d, const int32_t *indexes,
 }
 
 }  // extern "C"
+
+int dcvc_rans_set_threads(int workers) {
+  if (workers < 0 || workers > 64) return DCVC_EINVAL;
+  if (Pool::g_started.load()) return Pool::shared().workers() == workers ? DCVC_OK : DCVC_EBUSY;
+  Pool::g_threads = workers;
+  return DCVC_OK;
+}
+
+int dcvc_rans_threads(void) { return Pool::shared().workers(); }

@@ -9,7 +9,7 @@ import torch
 
 from .. import hip as K
 from ..hip import F32, ACT_LRELU, ACT_CLAMP01
-from ..layers import split_guarded, Ctx, Precision, DepthConvBlock, ResidualBlockWithStride, ResidualBlockUpsample, UNet
+from ..layers import split_guarded, split_checkpoint, Ctx, Precision, DepthConvBlock, ResidualBlockWithStride, ResidualBlockUpsample, UNet
 from ..entropy import ScaleTable, FactorizedTable, EntropyCoder
 from ..stream_helper import get_downsampled_shape, encode_i, decode_i, filesize, get_state_dict
 from .common import SymbolBuffer, QuadtreePrior, BitCounter, bits_result, pad_for_y, crop_to, q_fine, curr_q
@@ -21,6 +21,8 @@ class IntraNoAR:
                  device=None):
         self.N = N
         self.ec_thread, self.stream_part = ec_thread, stream_part
+        self._init_kw = dict(N=N, anchor_num=anchor_num, ec_thread=ec_thread, stream_part=stream_part,
+                             inplace=inplace)
         self.prec = precision if precision is not None else Precision.split()
         self.dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
         self.entropy_coder = None
@@ -188,8 +190,10 @@ class IntraNoAR:
             return {"bit": enc["bit"], "x_hat": enc["x_hat"]}
         assert pic_height is not None and pic_width is not None
         enc = self.compress(x, q_in_ckpt, q_index)
+        split_checkpoint(self, "compress")   # before the file is written
         encode_i(pic_height, pic_width, q_in_ckpt, q_index, enc["bit_stream"], output_path)
         bit = filesize(output_path) * 8
         height, width, q_in_ckpt, q_index, bit_stream = decode_i(output_path)
         dec = self.decompress(bit_stream, height, width, q_in_ckpt, q_index)
+        split_checkpoint(self, "decompress")
         return {"bit": bit, "x_hat": dec["x_hat"].nchw_view()}

@@ -15,7 +15,7 @@ import torch
 
 from .. import hip as K
 from ..hip import F32, ACT_LRELU, ACT_CLAMP01
-from ..layers import (split_guarded, Ctx, Precision, DepthConvBlock, ResidualBlockWithStride, ResidualBlockUpsample,
+from ..layers import (split_guarded, split_checkpoint, Ctx, Precision, DepthConvBlock, ResidualBlockWithStride, ResidualBlockUpsample,
                       ResBlock, UNet, SpyNet, Grids, hyper_enc, hyper_dec, cast)
 from ..entropy import ScaleTable, FactorizedTable, EntropyCoder
 from ..stream_helper import (get_downsampled_shape, encode_p, decode_p, filesize, get_state_dict)
@@ -47,6 +47,7 @@ class DMC:
                  device=None):
         self.anchor_num = anchor_num
         self.ec_thread, self.stream_part = ec_thread, stream_part
+        self._init_kw = dict(anchor_num=anchor_num, ec_thread=ec_thread, stream_part=stream_part, inplace=inplace)
         self.prec = precision if precision is not None else Precision.split()
         self.dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
         self.entropy_coder = None
@@ -429,12 +430,14 @@ class DMC:
         torch.cuda.current_stream(self.dev).synchronize()
         t0 = time.time()
         enc = self.compress(x, dpb, q_in_ckpt, q_index, frame_idx)
+        split_checkpoint(self, "compress")   # before the file is written
         encode_p(enc["bit_stream"], q_in_ckpt, q_index, frame_idx, output_path)
         bits = filesize(output_path) * 8
         torch.cuda.current_stream(self.dev).synchronize()
         t1 = time.time()
         q_in_ckpt, q_index, frame_idx, string = decode_p(output_path)
         dec = self.decompress(dpb, string, pic_height, pic_width, q_in_ckpt, q_index, frame_idx)
+        split_checkpoint(self, "decompress")
         torch.cuda.current_stream(self.dev).synchronize()
         t2 = time.time()
         return {"dpb": dec["dpb"], "bit": bits, "encoding_time": t1 - t0, "decoding_time": t2 - t1}

@@ -9,7 +9,7 @@ import torch
 
 from .. import hip as K
 from ..hip import F32, ACT_CLAMP01
-from ..layers import split_guarded, Ctx, Precision, hyper_enc, hyper_dec
+from ..layers import split_guarded, split_checkpoint, Ctx, Precision, hyper_enc, hyper_dec
 from ..entropy import ScaleTable, FactorizedTable
 from ..stream_helper import get_downsampled_shape, filesize, get_state_dict
 from ..dc.common import SymbolBuffer, BitCounter, bits_result
@@ -23,6 +23,7 @@ class IntraNoAR:
     def __init__(self, N=192, anchor_num=4, precision=None, device=None):
         self.N = N
         self.anchor_num = anchor_num
+        self._init_kw = dict(N=N, anchor_num=anchor_num)
         self.prec = precision if precision is not None else Precision.split()
         self.dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
         self.entropy_coder = None
@@ -152,8 +153,10 @@ class IntraNoAR:
         assert pic_height is not None and pic_width is not None
         q_scale, q_index = get_rounded_q(q_scale)
         enc = self.compress(x, q_scale)
+        split_checkpoint(self, "compress")   # before the file is written
         encode_i(pic_height, pic_width, q_index, enc["bit_stream"], output_path)
         bit = filesize(output_path) * 8
         height, width, q_index, bit_stream = decode_i(output_path)
         dec = self.decompress(bit_stream, height, width, q_index / 100)
+        split_checkpoint(self, "decompress")
         return {"bit": bit, "x_hat": dec["x_hat"].nchw_view()}

@@ -15,7 +15,7 @@ import torch
 
 from .. import hip as K
 from ..hip import F32, ACT_LRELU, ACT_CLAMP01
-from ..layers import split_guarded, Ctx, Precision, SpyNet, Grids, ResidualBlockWithStride, hyper_enc, hyper_dec
+from ..layers import split_guarded, split_checkpoint, Ctx, Precision, SpyNet, Grids, ResidualBlockWithStride, hyper_enc, hyper_dec
 from ..entropy import ScaleTable, FactorizedTable
 from ..stream_helper import get_downsampled_shape, filesize, get_state_dict
 from ..dc.common import SymbolBuffer, BitCounter, bits_result
@@ -30,6 +30,7 @@ CH_MV, CH_N, CH_M = 64, 64, 96  # video_model.py:140-142
 class DMC:
     def __init__(self, anchor_num=4, precision=None, device=None):
         self.anchor_num = anchor_num
+        self._init_kw = dict(anchor_num=anchor_num)
         self.prec = precision if precision is not None else Precision.split()
         self.dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
         self.entropy_coder = None
@@ -343,11 +344,13 @@ class DMC:
         mv_y_q_scale, mv_y_q_index = get_rounded_q(mv_y_q_scale)
         y_q_scale, y_q_index = get_rounded_q(y_q_scale)
         enc = self.compress(x, dpb, mv_y_q_scale, y_q_scale)
+        split_checkpoint(self, "compress")   # before the file is written
         encode_p(enc["bit_stream"], mv_y_q_index, y_q_index, output_path)
         bits = filesize(output_path) * 8
         mv_y_q_index, y_q_index, string = decode_p(output_path)
         torch.cuda.current_stream(self.dev).synchronize()
         start = time.time()
         dec = self.decompress(dpb, string, pic_height, pic_width, mv_y_q_index / 100, y_q_index / 100)
+        split_checkpoint(self, "decompress")
         torch.cuda.current_stream(self.dev).synchronize()
         return {"dpb": dec["dpb"], "bit": bits, "decoding_time": time.time() - start}

@@ -86,6 +86,8 @@ HIP_SYMBOLS = [
     ("dcvc_dwconv3x3", _i, [_T, _T, _vp, _vp, _vp]),
     ("dcvc_flow_warp", _i, [_T, _T, _T, _vp, _vp, _vp]),
     ("dcvc_offset_diversity", _i, [_T, _T, _T, _T, _vp, _vp, _vp, _vp, _f, _vp]),
+    ("dcvc_offset_diversity_workspace", ctypes.c_int64, [_i, _i]),
+    ("dcvc_offset_diversity_ws", _i, [_T, _T, _T, _T, _vp, _vp, _vp, _vp, _f, _vp, ctypes.c_int64, _vp]),
     ("dcvc_resize2x", _i, [_T, _T, _i, _f, _vp]),
     ("dcvc_pool2x2", _i, [_T, _T, _i, _vp]),
     ("dcvc_add", _i, [_T, _T, _T, _vp]),
@@ -183,13 +185,31 @@ class SplitRangeError(NativeError):
 def split_guard_arm(device):
     """Arm the fp16 range guard of the split kernels for the calling host
     thread (one device int32 flag per thread and device; the kernels launched
-    from this thread raise it)."""
+    from this thread raise it).  The flag is cleared (stream-ordered before
+    the kernels it guards), so a value left by an earlier, unguarded call can
+    never be charged to this one."""
     g = getattr(_tls, "split_flag", None)
     if g is None or g.device != device:
         g = torch.zeros(1, dtype=torch.int32, device=device)
         _tls.split_flag = g
-        check(lib().dcvc_split_range_flag(g.data_ptr()), "split_range_flag")
+    else:
+        g.zero_()
+    check(lib().dcvc_split_range_flag(g.data_ptr()), "split_range_flag")
     return g
+
+
+def split_guard_disarm():
+    """Stop the calling thread's split kernels from writing a flag (kernels
+    launched outside a guarded call then write nothing; the pointer of a
+    flag on another device is never left behind)."""
+    check(lib().dcvc_split_range_flag(None), "split_range_flag")
+
+
+def split_guard_tripped():
+    """Whether a split kernel launched from this thread since the last arm
+    saw |v| >= 2^15 (synchronises the current stream)."""
+    g = getattr(_tls, "split_flag", None)
+    return g is not None and bool(int(g.item()))
 
 
 def split_guard_check(what="frame"):
@@ -624,13 +644,25 @@ def flow_warp(x, flow, grid, y=None):
     return y
 
 
+OD_PLANAR = False  # fp32 OffsetDiversity through the group-planar kernel pair (A/B switch)
+
+
 def offset_diversity(feat, offs_half, flow, fw, fb, grid, y=None, max_mag=40.0):
     if y is None:
         y = empty(feat.H, feat.W, 48, feat.dtype, feat.buf.device)
     gx, gy = grid
     e0 = _t0()
-    check(lib().dcvc_offset_diversity(feat.c(), offs_half.c(), flow.c(), y.c(), fw.data_ptr(), fb.data_ptr(),
-                                      gx.data_ptr(), gy.data_ptr(), max_mag, stream()), "offset_diversity")
+    if feat.dtype == F32 and OD_PLANAR:
+        # fp32 maps: the group-planar kernel pair, with a stream-ordered
+        # workspace from torch's caching allocator (the feature's planar copy)
+        n = int(lib().dcvc_offset_diversity_workspace(y.H, y.W))
+        ws = torch.empty(n // 4, dtype=torch.float32, device=y.buf.device)
+        check(lib().dcvc_offset_diversity_ws(feat.c(), offs_half.c(), flow.c(), y.c(), fw.data_ptr(), fb.data_ptr(),
+                                             gx.data_ptr(), gy.data_ptr(), max_mag, ws.data_ptr(), n, stream()),
+              "offset_diversity")
+    else:
+        check(lib().dcvc_offset_diversity(feat.c(), offs_half.c(), flow.c(), y.c(), fw.data_ptr(), fb.data_ptr(),
+                                          gx.data_ptr(), gy.data_ptr(), max_mag, stream()), "offset_diversity")
     _t1(e0, "offset_diversity", y.H * y.W * 48 * 20, y.H * y.W * (96 * _esz(feat.dtype) + 8),
         f"offset_diversity | {y.H}x{y.W}")
     return y

@@ -58,20 +58,73 @@ class Precision:
         return "fast" if self.latent_compute == F32 else "fast-bf16-tail"
 
 
+def split_checkpoint(codec, stage):
+    """Inside a guarded encode_decode (split_guarded): raise
+    hip.SplitRangeError now if a split kernel of this frame has seen a value
+    outside the split's range.  The codecs call it right after ``compress``
+    (before the stream file is written) and after ``decompress``."""
+    if codec.prec.feat_compute == F16X3 and getattr(codec, "_guard_on", False):
+        K.split_guard_check(f"{type(codec).__name__}.{stage}")
+
+
+def parity_twin(codec):
+    """The fp32 (Precision.parity) twin of a split codec, built once, lazily,
+    from the same state_dict and constructor arguments; it shares the codec's
+    entropy coder (same stream_part / ec_thread, same tables)."""
+    t = getattr(codec, "_parity_twin", None)
+    if t is None:
+        kw = dict(codec._init_kw, precision=Precision.parity(), device=codec.dev)
+        t = type(codec)(**kw).load_state_dict(codec.sd)
+        if codec.entropy_coder is not None:
+            t.update(force=True)
+        codec._parity_twin = t
+    if codec.entropy_coder is not None:
+        t.entropy_coder = codec.entropy_coder
+    return t
+
+
 def split_guarded(fn):
-    """encode_decode of a codec in Precision.split(): arm the fp16 range guard
-    of the split kernels (dcvc_split_range_flag) for the calling thread before
-    the frame and check it after, raising hip.SplitRangeError instead of
-    returning a frame whose split operands saturated."""
+    """encode_decode of a codec in Precision.split(): the fp16 range guard of
+    the split kernels (dcvc_split_range_flag) is armed (and cleared) for the
+    calling thread for the frame, checked by the codec after ``compress``
+    (before the file is written) and after ``decompress``
+    (``split_checkpoint``), and disarmed on the way out whatever happens.
+
+    A frame that trips it is coded again, whole, by the codec's fp32 twin
+    (``parity_twin``: the same state_dict on the fp32 HIP kernels, the
+    reference's own arithmetic), so a drop-in run of an input the split cannot
+    carry (DCVC-HEM's random init grows its latents, common_model.py:32-37)
+    still gets a valid stream: write mode rewrites the same output file, and
+    the result dict says ``precision_fallback: "parity"``.  The encoder and
+    the decoder of a frame always run in one precision."""
     import functools
 
     @functools.wraps(fn)
     def run(self, *args, **kw):
         if self.prec.feat_compute != F16X3:
             return fn(self, *args, **kw)
+        ec = self.entropy_coder
+        trace = getattr(ec, "trace", None) if ec is not None else None
+        n0 = len(trace) if trace is not None else 0
         K.split_guard_arm(self.dev)
-        out = fn(self, *args, **kw)
-        K.split_guard_check(f"{type(self).__name__}.encode_decode")
+        self._guard_on = True
+        try:
+            out = fn(self, *args, **kw)
+            K.split_guard_check(f"{type(self).__name__}.encode_decode")
+            return out
+        except K.SplitRangeError as e:
+            reason = str(e)
+        finally:
+            self._guard_on = False
+            K.split_guard_disarm()
+        # the fp32 twin codes the frame again (its encoder and decoder);
+        # the coder trace keeps only the twin's calls
+        if trace is not None:
+            del trace[n0:]
+        self.fallbacks = getattr(self, "fallbacks", 0) + 1
+        out = parity_twin(self).encode_decode(*args, **kw)
+        out["precision_fallback"] = "parity"
+        out["precision_fallback_reason"] = reason
         return out
     return run
 

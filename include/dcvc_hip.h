@@ -233,6 +233,18 @@ int dcvc_offset_diversity(dcvc_tensor feat, dcvc_tensor offs_half,
                           const float *fb, const float *gx, const float *gy,
                           float max_mag, void *stream);
 
+/* The same with a caller-provided device workspace of at least
+ * dcvc_offset_diversity_workspace(H, W) bytes (16-byte aligned): fp32 maps
+ * run the group-planar form (the feature copied to [16][H][W][3] in the
+ * workspace, one group per wave), identical results; anything else runs
+ * dcvc_offset_diversity. */
+int64_t dcvc_offset_diversity_workspace(int H, int W);
+int dcvc_offset_diversity_ws(dcvc_tensor feat, dcvc_tensor offs_half,
+                             dcvc_tensor flow, dcvc_tensor y, const float *fw,
+                             const float *fb, const float *gx, const float *gy,
+                             float max_mag, void *workspace, int64_t ws_bytes,
+                             void *stream);
+
 /* Bilinear resize by 2 (up) or 1/2 (down), align_corners=False
  * (bilinearupsacling / bilineardownsacling, video_net.py:41-55), followed by
  * a multiply (flow * 2.0, mv / 2). */

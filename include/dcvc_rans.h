@@ -122,6 +122,19 @@ int dcvc_rans_dec_decode_table_i32(dcvc_rans_dec *d, const int32_t *indexes,
                                    int64_t n, const dcvc_cdf_table *t,
                                    int32_t *out);
 
+/* ---- threads ---------------------------------------------------------------
+ * Every encoder and decoder of the process works its stream parts on one
+ * shared pool of persistent worker threads (plus the calling thread), not on
+ * threads of its own (the reference's RansEncoderLibMultiThread keeps one
+ * worker per encoder, rans.h:83-109, and RansDecoder starts one std::async
+ * per part per call, py_rans.cpp:197-211).  dcvc_rans_set_threads(n) fixes
+ * the worker count before the first coder is created (default: the
+ * DCVC_CODER_THREADS environment variable, else min(15, hardware threads - 1));
+ * afterwards it returns DCVC_EBUSY unless n is the running count.
+ * dcvc_rans_threads() starts the pool if needed and returns its workers. */
+int dcvc_rans_set_threads(int workers);
+int dcvc_rans_threads(void);
+
 #ifdef __cplusplus
 }
 #endif

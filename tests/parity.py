@@ -131,6 +131,10 @@ def check_forced(sf, bits, bits_replay, psnr, psnr_replay, name=""):
     assert not sf["unexplained"], msg
     if sf["identical"]:
         assert bits == bits_replay, msg
+    if "bits_replay_tied" in sf:
+        # symbols all agree: the replay coded with the product's decisions at
+        # its index ties is the product's stream
+        assert bits == sf["bits_replay_tied"], msg + f", replay with the product's tie indexes {sf['bits_replay_tied']}"
     assert abs(psnr - psnr_replay) < PSNR_DB, msg
     return msg
 

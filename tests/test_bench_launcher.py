@@ -10,14 +10,35 @@ import sys
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def test_bench_gpus_2_launches_two_ranks():
+import pytest
+
+
+@pytest.mark.parametrize("n", [2, 8])
+def test_bench_gpus_n_launches_n_ranks(n):
+    """--gpus N (2, and the driver's 8) starts N ranks that join, reduce and
+    report; every rank takes a disjoint core share (rank_cpu_plan on two
+    synthetic NUMA nodes) and sizes the shared rANS pool to it, so a rank runs
+    at most lanes + stream_part coder threads (GOP lane threads + pool
+    workers), however many coders its lanes create."""
     env = dict(os.environ)
     env.pop("WORLD_SIZE", None)
     env["CUDA_VISIBLE_DEVICES"] = ""
-    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--launcher-selftest"],
-                       capture_output=True, text=True, timeout=240, env=env, cwd=REPO)
+    env["OMP_NUM_THREADS"] = "1"
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", str(n), "--launcher-selftest"],
+                       capture_output=True, text=True, timeout=600, env=env, cwd=REPO)
     assert r.returncode == 0, r.stderr[-2000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, r.stdout
     d = json.loads(lines[0])
-    assert d["n_gpus"] == 2 and d["ranks_joined"] == 2 and d["rank_sum"] == 1 and d["requested"] == 2
+    assert d["n_gpus"] == n and d["ranks_joined"] == n and d["rank_sum"] == n * (n - 1) // 2 and d["requested"] == n
+    shares = [set(p["share"]) for p in d["plans"]]
+    ncpu = len(os.sched_getaffinity(0))
+    if ncpu >= n:
+        for i in range(n):
+            for j in range(i + 1, n):
+                assert not shares[i] & shares[j], (i, j, d["plans"])
+    for p in d["plans"]:
+        assert p["set_rc"] == 0 and 1 <= p["coder_workers"] <= 8 - 1, p
+        assert p["coders"] == 2 * 3
+        # (lane threads are the bench's own; the selftest counts the pool)
+        assert p["coder_workers"] <= max(1, len(p["share"]) - 3) or p["coder_workers"] == 1, p

@@ -913,3 +913,38 @@ def test_offset_diversity_paired_bf16_loads_bit_identical(H, W):
     y2 = h.offset_diversity(wide.ch(1, 48), oa, fl, fw, fb, _grid(H, W))
     torch.cuda.synchronize()
     assert torch.equal(y1.t().cpu(), y2.t().cpu())
+
+
+@pytest.mark.parametrize("H,W,oscale", [(6, 2, 0.05), (10, 18, 0.05), (24, 130, 2.0), (68, 256, 0.5),
+                                        (1088, 1920, 0.05)])
+def test_offset_diversity_planar_bit_identical(H, W, oscale):
+    """fp32 OffsetDiversity: the group-planar kernel pair (feature copied to
+    [16][H][W][3], one group per wave, offsets and outputs staged in LDS;
+    dcvc_offset_diversity_ws) gives the pixel-major kernel's bits, on the
+    codec's views (input a wider buffer's channel window, output written into
+    the 96-channel concat buffer at channel 48), with widths that are not a
+    multiple of its 64-pixel runs and offsets large enough to clamp at the
+    borders (oscale 2: 40 tanh(o) near +-40 pixels)."""
+    h = K()
+    g = torch.Generator().manual_seed(H * 7 + W)
+    feat = torch.randn(1, 48, H, W, generator=g)
+    flow = torch.randn(1, 2, H, W, generator=g) * 3
+    offs = torch.randn(1, 96, H // 2, W // 2, generator=g) * oscale
+    fw = (torch.randn(48, 6, generator=g) * 0.3).contiguous().cuda()
+    fb = (torch.randn(48, generator=g) * 0.1).cuda()
+    wide = h.zeros(H, W, 56, h.F32)
+    h.copy(to_act(feat, h.F32), wide.ch(4, 48))
+    fa = wide.ch(4, 48)
+    oa, fl = to_act(offs, h.F32), to_act(flow, h.F32)
+    gx, gy = _grid(H, W)
+    y_ref = h.zeros(H, W, 96, h.F32)
+    h.check(h.lib().dcvc_offset_diversity(fa.c(), oa.c(), fl.c(), y_ref.ch(48, 48).c(), fw.data_ptr(), fb.data_ptr(),
+                                          gx.data_ptr(), gy.data_ptr(), 40.0, h.stream()), "od")
+    y = h.zeros(H, W, 96, h.F32)
+    old, h.OD_PLANAR = h.OD_PLANAR, True
+    try:
+        h.offset_diversity(fa, oa, fl, fw, fb, (gx, gy), y=y.ch(48, 48))
+    finally:
+        h.OD_PLANAR = old
+    torch.cuda.synchronize()
+    assert torch.equal(y.t().cpu(), y_ref.t().cpu())

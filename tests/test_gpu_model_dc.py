@@ -25,6 +25,13 @@ pytestmark = pytest.mark.gpu
 # max fraction of symbols differing from the oracle, max |bits - oracle| / oracle,
 # max |PSNR - oracle PSNR| in dB (random-weight sequences, PSNR ~6-7 dB)
 PARITY_TOL = {"sym_frac": 2e-3, "bits_rel": 5e-3, "psnr_db": 1e-4}
+# split precision (the bench's) in estimate mode: the float bit estimates of
+# the free-running golden sequences, measured within 4e-7 of the reference's
+# (gpurun_out/parity_dc.json estimate_split_*); 1e-5 leaves no room for a
+# regression of the estimate path.  Parity mode keeps PARITY_TOL: its fp32
+# chain flips one tie of golden B frame 1 and frame 2 then codes a slightly
+# different picture (1.1e-3), as the reference does at another thread count
+SPLIT_EST_TOL = {"bits_rel": 1e-5, "psnr_db": 1e-4}
 FAST_TOL = {"sym_frac": 0.05, "bits_rel": 0.02, "psnr_db": 0.05}
 
 OUT = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "gpurun_out")
@@ -218,7 +225,7 @@ def test_estimate_mode_vs_reference(dc_golden, oracle_est, tag, mode):
     precision) and parity are held to PARITY_TOL, fast (bf16) to FAST_TOL."""
     from dcvc_amd.layers import Precision
     prec = getattr(Precision, mode)()
-    tol = FAST_TOL if mode == "fast" else PARITY_TOL
+    tol = {"fast": FAST_TOL, "split": SPLIT_EST_TOL}.get(mode, PARITY_TOL)
     prod = run_product_estimate(dc_golden, tag, prec)
     stats = []
     for t, (a, b) in enumerate(zip(prod, oracle_est[tag])):

@@ -75,6 +75,14 @@ class Pair:
         stream = self.R.DCStream().encode(cc)
         return calls, tap, (len(stream) + (13 if t == 0 else 6)) * 8, dpb
 
+    def coded_bits(self, t, calls):
+        """Bits of a frame's calls [(kind, symbols, indexes)] through the
+        oracle's coder, with the stream headers encode_i / encode_p add."""
+        pre = "i_" if t == 0 else "p_"
+        cc = [(np.clip(np.asarray(s).reshape(-1).astype(np.int64), -30000, 30000).astype(np.int16),
+               np.asarray(ix).reshape(-1).astype(np.int16), self.tabs[pre + k]) for k, s, ix in calls]
+        return (len(self.R.DCStream().encode(cc)) + (13 if t == 0 else 6)) * 8
+
     def product(self, t, xp, dpb_o, q, fidx, path, h, w):
         net = self.pi if t == 0 else self.pp
         net.entropy_coder.trace = []
@@ -120,6 +128,13 @@ def run_teacher_forced(pair, frames, q, h, w, name):
                 sf = compare_forced(enc, calls_f, tap_f, fr.forced)
                 p_f = psnr(dpb_f["ref_frame"][:, :, :h, :w], x)
                 sf.update({"bits_replay": int(bits_f), "psnr_replay": p_f})
+                if sf["sym_diff"] == 0:
+                    # every symbol agrees and every differing index is a tie
+                    # of the replay (compare_forced): the replay's stream with
+                    # the product's index at those ties must be the product's
+                    # stream, to the bit
+                    sf["bits_replay_tied"] = pair.coded_bits(
+                        t, [(c[0], ps, pi) for c, (ps, pi) in zip(calls_f, enc)])
                 st["replay"] = sf
                 msg += "\n" + check_forced(sf, bits, bits_f, p, p_f, f"{name} t={t}")
             stats.append((st, msg))
@@ -179,33 +194,45 @@ def test_strict_parity_c3small_survey_recipe(prec):
             assert st["bits"] == want, msg
 
 
+# (h, w, frames): 1080p I + P, and C4's own 3840x2160 (latent grid 135x240,
+# hyperprior pad to 136x240, 4K tile counts).  At 4K the oracle takes about a
+# minute per I-frame on 16 host threads and three per P-frame, so the GPU
+# suite codes the I-frame there; DCVC_C4_4K_P=1 adds the P-frame
+# (profiles/r05*_parity_strict.json records a run with it)
+C4_SIZES = {"1080p": (1080, 1920, 2), "2160p": (2160, 3840, 2 if os.environ.get("DCVC_C4_4K_P") == "1" else 1)}
+
+
+@pytest.mark.parametrize("size", ["1080p", "2160p"])
 @pytest.mark.parametrize("prec", ["split"])
-def test_strict_parity_c4_yuv420(prec):
+def test_strict_parity_c4_yuv420(prec, size):
     """The C4 path (DCVC-DC on YUV420 input, test_video.py:110-195 with
-    src_type yuv420: 4:2:0 planes upsampled to 4:4:4 YCbCr and replicate-padded
-    on the GPU) at 1920x1080 in the bench's split precision: the GPU-converted
-    input equals the oracle's conversion bit for bit, then an I-frame and a
-    P-frame are held to the strict bar.  (The 4K size of C4 runs lossless in
-    tests/test_gpu_configs.py; its oracle would take minutes per frame.)"""
+    src_type yuv420: 4:2:0 planes upsampled to 4:4:4 YCbCr and padded to a
+    multiple of 16 on the GPU; 2160 and 3840 need none) in the bench's split
+    precision: the GPU-converted input equals the oracle's conversion bit for
+    bit, then the frames are held to the strict bar, at 1080p and at C4's own
+    3840x2160 (DCVC-DC/src/models/common_model.py:70-86: pad_for_y /
+    slice_to_y of the 135x240 latent grid)."""
     import bench
     from dcvc_amd.harness import FrameStage
     from dcvc_amd.synth import moving_pattern_yuv420
     from oracle.harness_oracle import yuv_u8_to_input
     isd, psd = bench.make_weights(None, 0, torch.device("cpu"), "dc")
-    h, w = 1080, 1920
-    H, W = 1088, 1920
+    h, w, nf = C4_SIZES[size]
+    H, W = (h + 15) // 16 * 16, (w + 15) // 16 * 16
     dev = torch.device("cuda", 0)
-    stage = FrameStage(h, w, 16, True, zero_pad=False, frame_num=2, device=dev)
+    stage = FrameStage(h, w, 16, True, zero_pad=False, frame_num=nf, device=dev)
     frames = []
-    for t in range(2):
+    for t in range(nf):
         y, uv = moving_pattern_yuv420(h, w, t, seed=1)
         xo = torch.from_numpy(yuv_u8_to_input(y, uv, H, W)).permute(2, 0, 1).unsqueeze(0).contiguous()
         xg = stage.load((torch.from_numpy(y).to(dev), torch.from_numpy(uv).to(dev)))
         xg = xg.nchw() if hasattr(xg, "nchw") else xg
         assert torch.equal(xg.float().cpu(), xo), "GPU YUV420 -> 4:4:4 input differs from the oracle's"
         frames.append((xo[:, :, :h, :w], xo))
+        del xg
     pair = Pair(isd, psd, prec)
-    stats = run_teacher_forced(pair, frames, 0, h, w, f"C4path_yuv420_1080p_{prec}")
+    name = f"C4path_yuv420_1080p_{prec}" if size == "1080p" else f"C4_yuv420_2160p_{prec}"
+    stats = run_teacher_forced(pair, frames, 0, h, w, name)
     for st, msg in stats:
         print(msg)
 
@@ -270,6 +297,10 @@ class HemPair(Pair):
             out.append((kind, sym.reshape(-1), idx))
         nbytes = self._stream_bytes([(k, s.int().numpy(), i.numpy()) for k, s, i in out])
         return out, tap, (nbytes + (14 if t == 0 else 8)) * 8, dpb
+
+    def coded_bits(self, t, calls):
+        return (self._stream_bytes([(k, np.asarray(s).astype(np.int32), np.asarray(i)) for k, s, i in calls])
+                + (14 if t == 0 else 8)) * 8
 
     def product(self, t, xp, dpb_o, q, fidx, path, h, w):
         qi, qmv, qy = self.q

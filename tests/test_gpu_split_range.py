@@ -104,3 +104,113 @@ def test_codec_frame_in_range_does_not_raise(dc_golden):
         r = net.encode_decode(xp.cuda(), False, 40, os.path.join(td, "i.bin"), pic_width=x.shape[3],
                               pic_height=x.shape[2])
     assert r["bit"] > 0
+
+
+# (parameter pair, stage that trips): conv A's weights and bias times 2^16,
+# conv B's weights times 2^-16, leaky ReLU between them.  In fp32 arithmetic
+# scaling by a power of two is exact and a leaky ReLU commutes with it, so
+# the network's output is bit for bit that of the unscaled weights while A's
+# output (B's input) leaves the split's range (|v| >= 2^15)
+HOT_PAIRS = {
+    "compress": ("y_prior_fusion.0", "y_prior_fusion.2"),
+    "decompress": ("contextual_decoder.res1.conv1", "contextual_decoder.res1.conv2"),
+}
+
+
+def _hot(sd, pair):
+    a, b = pair
+    out = dict(sd)
+    out[a + ".weight"] = sd[a + ".weight"] * 65536.0
+    out[a + ".bias"] = sd[a + ".bias"] * 65536.0
+    out[b + ".weight"] = sd[b + ".weight"] / 65536.0
+    return out
+
+
+@pytest.mark.parametrize("stage", ["compress", "decompress"])
+def test_hem_frame_out_of_range_falls_back(stage):
+    """A whole DCVC-HEM P-frame (golden sequence A) whose activations pass
+    2^15 (DCVC-HEM/src/models/common_model.py:32-37: the reference codes any
+    fp32 range): the split codec does not abort or leave a stream of a failed
+    attempt behind; the frame is coded again by its fp32 twin, the output file
+    holds that stream, its decode is lossless, and the frame meets the strict
+    teacher-forced bar against the oracle run on the unscaled weights (the
+    same function, test docstring above)."""
+    import os
+    import tempfile
+    import numpy as np
+    from tests.hem_fixtures import HEMGolden
+    from tests.test_gpu_parity_strict import HemPair
+    from tests.parity import compare_frame, check_frame
+    from tests.test_gpu_parity_strict import psnr
+    from dcvc_amd.hem import DMC
+    from dcvc_amd.layers import Precision
+    g = HEMGolden()
+    meta = g.meta["A"]
+    h, w = meta["h"], meta["w"]
+    psd = g.p_state_dict()
+    pair = HemPair(g.i_state_dict(), psd, g.q("A"), "split")
+    hot = DMC(precision=Precision.split()).load_state_dict(_hot(psd, HOT_PAIRS[stage]))
+    hot.update(force=True)
+    ref = DMC(precision=Precision.parity()).load_state_dict(psd)   # the twin's arithmetic, unscaled weights
+    ref.update(force=True)
+    frames = [g.frame_tensor("A", t) for t in range(2)]
+    _, tap0, _, dpb_o = pair.oracle(0, frames[0][1], None, None, 0)
+    x, xp = frames[1]
+    calls, tap, bits_o, dpb_next = pair.oracle(1, xp, dpb_o, None, 1)
+    with tempfile.TemporaryDirectory() as td:
+        res = {}
+        for name, net in (("hot", hot), ("ref", ref)):
+            pair.pp = net
+            path = os.path.join(td, f"{name}.bin")
+            enc, bits, rec = pair.product(1, xp, dpb_o, None, 1, path, h, w)   # asserts decoder == encoder
+            r_fb = getattr(net, "fallbacks", 0)
+            res[name] = (enc, bits, rec, os.path.getsize(path) * 8, r_fb)
+    enc, bits, rec, fbits, nfb = res["hot"]
+    assert nfb == 1, "the split codec did not fall back"
+    assert fbits == bits, "the output file is not the stream the frame reports"
+    enc_r, bits_r, rec_r, _, _ = res["ref"]
+    # the fallback IS the fp32 path: same calls, bits and reconstruction
+    assert bits == bits_r
+    for (s1, i1), (s2, i2) in zip(enc, enc_r):
+        np.testing.assert_array_equal(s1.reshape(-1), s2.reshape(-1))
+        np.testing.assert_array_equal(i1.reshape(-1), i2.reshape(-1))
+    assert torch.equal(rec.cpu(), rec_r.cpu())
+    st = compare_frame(enc, calls, tap)
+    check_frame(st, bits, bits_o, psnr(rec[:, :, :h, :w], x), psnr(dpb_next["ref_frame"][:, :, :h, :w], x),
+                f"hem_A fallback ({stage})")
+
+
+def test_guard_cleared_between_calls(dc_golden):
+    """an unguarded split call that leaves the range (a direct
+    kernel call here) must not be charged to the next guarded frame: arming
+    clears the flag, and a guarded call disarms it on the way out."""
+    import tempfile
+    import os
+    from dcvc_amd.dc import IntraNoAR
+    from dcvc_amd.layers import Precision
+    h = K()
+    dev = torch.device("cuda", 0)
+    h.split_guard_arm(dev)
+    h.split_guard_disarm()
+    # out of range with the guard off: nothing may be recorded
+    x = torch.full((1, 48, 16, 16), 1.0e5)
+    cw = h.ConvW(torch.randn(48, 48, 3, 3) * 0.01, torch.zeros(48), 1, h.F16X3)
+    h.conv(cw, h.from_nchw(x, h.F32), out_dtype=h.F32)
+    torch.cuda.synchronize()
+    assert not h.split_guard_tripped()
+    # out of range with a stale armed flag, then a guarded in-range frame
+    h.split_guard_arm(dev)
+    h.conv(cw, h.from_nchw(x, h.F32), out_dtype=h.F32)
+    torch.cuda.synchronize()
+    assert h.split_guard_tripped()
+    net = IntraNoAR(precision=Precision.split()).load_state_dict(dc_golden.i_state_dict())
+    net.update(force=True)
+    xf, xp = dc_golden.frame_tensor("B", 0)
+    with tempfile.TemporaryDirectory() as td:
+        r = net.encode_decode(xp.cuda(), False, 40, os.path.join(td, "i.bin"), pic_width=xf.shape[3],
+                              pic_height=xf.shape[2])
+    assert "precision_fallback" not in r and getattr(net, "fallbacks", 0) == 0
+    # the guarded call disarmed the flag on its way out
+    h.conv(cw, h.from_nchw(x, h.F32), out_dtype=h.F32)
+    torch.cuda.synchronize()
+    assert not h.split_guard_tripped()

@@ -171,3 +171,53 @@ def test_reference_coder_inputs_roundtrip_byte_exact(dc_golden):
             dec.set_stream(stream)
             for name, s, i in calls:
                 np.testing.assert_array_equal(dec.decode_table(i, tabs[name]), s.reshape(-1))
+
+
+def _nthreads():
+    return len(os.listdir("/proc/self/task"))
+
+
+def test_shared_pool_concurrent_coders_byte_exact():
+    """All coders of a process share one worker pool (dcvc_rans_set_threads /
+    dcvc_rans_threads): creating many multi-part coders adds no threads, and
+    six host threads coding 8-part streams at once (GOP lanes x I/P codecs)
+    each get the oracle's bytes and a lossless decode."""
+    import threading
+    from dcvc_amd._native import rans_lib
+    L = rans_lib()
+    workers = L.dcvc_rans_threads()
+    assert 0 <= workers <= 64
+    assert L.dcvc_rans_set_threads(workers) == 0
+    assert L.dcvc_rans_set_threads(workers + 1) == -5   # running pool: DCVC_EBUSY
+    tab = laplace_table()
+    ct = P.CdfTable(*tab)
+    base = _nthreads()
+    coders = [(P.RansEncoder(True, 8), P.RansDecoder(8)) for _ in range(12)]
+    assert _nthreads() == base, "coders must not start threads of their own"
+    jobs = []
+    for k in range(6):
+        s, i = symbols(20000 + 977 * k, tab[0].shape[0], 100 + k, wide=(k % 3 == 0))
+        jobs.append((s, i, R.DCStream(8).encode([(s, i, tab)])))
+    errors = []
+
+    def lane(k):
+        enc, dec = coders[k]
+        s, i, want = jobs[k]
+        try:
+            for _ in range(8):
+                enc.reset()
+                enc.encode_table(s, i, ct)
+                enc.flush()
+                got = enc.get_encoded_stream()
+                assert got.tobytes() == want
+                dec.set_stream(got)
+                np.testing.assert_array_equal(dec.decode_table(i, ct), np.where(i >= 0, s, 0))
+        except Exception as e:  # noqa: BLE001
+            errors.append((k, repr(e)))
+    th = [threading.Thread(target=lane, args=(k,)) for k in range(6)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errors, errors
+    assert _nthreads() == base
