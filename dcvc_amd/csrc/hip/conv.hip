@@ -588,6 +588,9 @@ extern "C" void dcvc_internal_sgemm_pd(int v);
 extern "C" int dcvc_internal_set_option_split(const char *name, int value);
 extern "C" int dcvc_internal_xconv(const dcvc_conv_args *a, void *stream);
 extern "C" void dcvc_internal_xconv_enable(int v);
+extern "C" int dcvc_internal_dconv(const dcvc_conv_args *a, void *stream);
+extern "C" void dcvc_internal_dconv_enable(int v);
+extern "C" void dcvc_internal_dconv_1x1(int v);
 
 // fp16 range guard of the split kernels (split.h SplitRange): one flag per
 // calling host thread (concurrent GOP lanes each launch from their own thread
@@ -653,7 +656,9 @@ extern "C" int dcvc_conv2d(const dcvc_conv_args *a, void *stream) {
     p.r2co = a->res2.coff;
   }
   if (a->compute == DCVC_F16X3) {   // the split-fp16 kernels only
-    const int r = dcvc_internal_xconv(a, stream);   // static-shape 3x3 stride-1 kernel (xconv.hip)
+    int r = dcvc_internal_xconv(a, stream);   // static-shape 3x3 stride-1 kernel (xconv.hip)
+    if (r != DCVC_HIP_EUNSUPPORTED) return r;
+    r = dcvc_internal_dconv(a, stream);       // stride 2 and narrow 7x7: direct operand loads (dconv.hip)
     if (r != DCVC_HIP_EUNSUPPORTED) return r;
     return dcvc_internal_sconv(a, stream);
   }
@@ -806,6 +811,14 @@ extern "C" int dcvc_set_option(const char *name, int value) {
   }
   if (std::strcmp(name, "xconv") == 0) {
     dcvc_internal_xconv_enable(value);
+    return DCVC_HIP_OK;
+  }
+  if (std::strcmp(name, "dconv") == 0) {
+    dcvc_internal_dconv_enable(value);
+    return DCVC_HIP_OK;
+  }
+  if (std::strcmp(name, "dconv_1x1") == 0) {
+    dcvc_internal_dconv_1x1(value);
     return DCVC_HIP_OK;
   }
   if (std::strcmp(name, "conv3x3_rows4") == 0) {

@@ -7,6 +7,9 @@
 #   smoke    __graft_entry__.smoke()
 #   micro    scripts/sconv_bench.py $MICRO_ARGS (kernel microbenchmarks)
 #   prof     rocprofv3 kernel stats of a one-lane bench
+#   ab       interleaved A/B of $AB_SHAPES (scripts/sconv_bench.py): the product library, then
+#            dcvc_amd/lib/$AB_LIB (DCVC_HIP_LIB), twice each, one JSON line per shape and arm
+#   bench1b  bench1 with DCVC_HIP_LIB=$AB_LIB
 #   block    scripts/block_bench.py $BLOCK_ARGS (fused blocks / gathers), repeated for $BLOCK_ARGS2 if set
 #   kstats   rocprofv3 kernel stats of: python $KSTATS_CMD
 #   pmc      SQ / LDS / MFMA and HBM counters (scripts/pmc_cmd.sh) of: python $PMC_CMD
@@ -25,8 +28,9 @@ for s in $STEPS; do
     tests)  timeout -k 10 1000 python -u -m pytest ${PYTEST_ARGS:-tests} -m gpu -x -q -p no:cacheprovider --timeout 600 \
               --timeout-method thread > gpurun_out/${TAG}_pytest.log 2>&1 ;;
     smoke)  timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${TAG}_smoke.log 2>&1 ;;
-    micro)  timeout -k 10 300 python -u scripts/sconv_bench.py ${MICRO_ARGS:-} > gpurun_out/${TAG}_micro.jsonl \
-              2> gpurun_out/${TAG}_micro.err ;;
+    micro)  { timeout -k 10 300 python -u scripts/sconv_bench.py ${MICRO_ARGS:-} &&
+              if [ -n "${MICRO_ARGS2:-}" ]; then timeout -k 10 300 python -u scripts/sconv_bench.py ${MICRO_ARGS2}; fi; } \
+              > gpurun_out/${TAG}_micro.jsonl 2> gpurun_out/${TAG}_micro.err ;;
     prof)   timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_prof -o run --output-format csv \
               -- python bench.py --lanes 1 --steps 6 --warmup 2 --no-cpu-baseline --no-roofline \
               > gpurun_out/${TAG}_prof.log 2>&1 ;;
@@ -36,6 +40,12 @@ for s in $STEPS; do
     kstats) timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_kstats -o run --output-format csv \
               -- python ${KSTATS_CMD} > gpurun_out/${TAG}_kstats.log 2>&1 ;;
     pmc)    bash scripts/pmc_cmd.sh gpurun_out/${TAG}_pmc python ${PMC_CMD} > gpurun_out/${TAG}_pmc.log 2>&1 ;;
+    ab)     { for rep in 1 2; do
+                timeout -k 10 300 python -u scripts/sconv_bench.py --shapes ${AB_SHAPES} --opt arm=A || exit 1
+                DCVC_HIP_LIB=${AB_LIB} timeout -k 10 300 python -u scripts/sconv_bench.py --shapes ${AB_SHAPES} --opt arm=B || exit 1
+              done; } > gpurun_out/${TAG}_ab.jsonl 2> gpurun_out/${TAG}_ab.err ;;
+    bench1b) DCVC_HIP_LIB=${AB_LIB} timeout -k 10 600 python bench.py --lanes 1 --steps 12 --warmup 3 --no-cpu-baseline \
+              --profile-out gpurun_out/${TAG}_layers_b.json ${BENCH_ARGS:-} > gpurun_out/${TAG}_bench1b.log 2>&1 ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
   rc=$?

@@ -33,7 +33,8 @@ def main():
     torch.manual_seed(0)
     for o in a.opt:
         name, val = o.split("=")
-        K.set_option(name, int(val))
+        if name != "arm":   # (a label only: which library of an A/B run)
+            K.set_option(name, int(val))
     for sh in a.shapes.split(","):
         m = re.fullmatch(r"(\d+)x(\d+)@(\d+)x(\d+)(?:k(\d))?(?:s(\d))?(r?)(u?)", sh)
         cin, cout, H, W = (int(m.group(i)) for i in range(1, 5))

@@ -23,13 +23,16 @@ def _gpu():
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     torch.manual_seed(0)
-    # these tests pin sconv.hip itself: the static-shape 3x3 kernel (xconv.hip)
-    # that takes its 3x3 stride-1 shapes first is compared with it bit for bit
-    # in test_gpu_xconv.py
+    # these tests pin sconv.hip / sgemm.hip themselves: the static-shape 3x3
+    # kernel (xconv.hip) and the direct kernel (dconv.hip) that take their
+    # shapes first are compared with them bit for bit in test_gpu_xconv.py /
+    # test_gpu_dconv.py
     from dcvc_amd import hip
     hip.set_option("xconv", 0)
+    hip.set_option("dconv", 0)
     yield
     hip.set_option("xconv", 1)
+    hip.set_option("dconv", 1)
 
 
 def K():

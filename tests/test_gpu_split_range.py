@@ -7,7 +7,8 @@ kernel raises the calling thread's flag when a value it splits reaches 2^15;
 the codecs check it once per frame (layers.split_guarded) and raise
 SplitRangeError.  Here: inputs just under the limit still match fp64 at the
 split bound; inputs around 1e5 raise, through every split kernel family (3x3
-static kernel, generic sconv, 1x1 sgemm, fused ConvFFN / DepthConv).
+static kernel, generic sconv, direct dconv (stride 2, 1x1, narrow 7x7), fused
+ConvFFN / DepthConv).
 """
 import pytest
 import torch
@@ -34,8 +35,9 @@ def rel_err(got, ref):
 
 
 # (cin, cout, k, stride, kernel family expected)
-CONVS = [(48, 48, 3, 1, "xconv3_kernel"), (6, 64, 3, 1, "sconv_kernel"), (56, 64, 3, 2, "sconv_kernel"),
-         (32, 64, 7, 1, "xconv3_kernel"), (8, 32, 7, 1, "sconv_kernel"), (96, 48, 1, 1, "sgemm_kernel")]
+CONVS = [(48, 48, 3, 1, "xconv3_kernel"), (6, 64, 3, 1, "sconv_kernel"), (56, 64, 3, 2, "dconv_kernel"),
+         (32, 64, 7, 1, "xconv3_kernel"), (8, 32, 7, 1, "sconv_kernel"), (96, 48, 1, 1, "sgemm_kernel"),
+         (64, 48, 3, 2, "dconv_kernel")]
 
 
 @pytest.mark.parametrize("case", CONVS)

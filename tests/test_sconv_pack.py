@@ -84,9 +84,10 @@ def test_pack_f16x3_rejects_out_of_range(bad):
 
 @pytest.mark.parametrize("c,hid", [(48, 192), (128, 512), (32, 128)])
 def test_ffn_pack_roundtrip(c, hid):
-    """dcvc_ffn_pack_weights: per hidden slice the swizzled LDS images of
-    ffn1 ([kc][h][32]) and ffn2 ([kc2][n][32]), hi then lo; decoded back they
-    give the weights to ~2^-22."""
+    """dcvc_ffn_pack_weights: per slice of 32 hidden channels the swizzled LDS
+    images of ffn1 ([kc][h][32]) and ffn2 ([n][32], its K order permuted to the
+    order ffn1's accumulators leave the hidden values in), hi then lo; decoded
+    back they give the weights to ~2^-22."""
     from dcvc_amd import hip as h
     g = torch.Generator().manual_seed(c)
     w1 = (torch.randn(hid, c, generator=g) / c ** 0.5).numpy().astype(np.float32)
@@ -96,15 +97,20 @@ def test_ffn_pack_roundtrip(c, hid):
     buf = np.zeros(n, dtype=np.uint16)
     assert h.lib().dcvc_ffn_pack_weights(w1.ctypes.data_as(vp), w2.ctypes.data_as(vp), c, hid,
                                          buf.ctypes.data_as(vp)) == n
-    HS = 32 if c >= 128 else 64
-    kc1, c16, kc2 = (c + 31) // 32, (c + 15) // 16 * 16, HS // 32
-    w1n, w2n = kc1 * HS * 32, kc2 * c16 * 32
+    HS = 32
+    kc1, c16 = (c + 31) // 32, (c + 15) // 16 * 16
+    w1n, w2n = kc1 * HS * 32, c16 * 32
     sl = 2 * w1n + 2 * w2n
     assert n == sl * (hid // HS)
 
     def at(row, k):
         x = (0x1320 >> (((row >> 2) & 3) << 2)) & 3
         return row * 32 + ((((k >> 3) ^ x) & 3) << 3) + (k & 7)
+
+    def perm(k):   # ffn2's K position 8 q + m holds hidden channel 4 q + m / 16 + 4 q + m - 4
+        q, m = k >> 3, k & 7
+        return 4 * q + m if m < 4 else 16 + 4 * q + m - 4
+    assert sorted(perm(k) for k in range(32)) == list(range(32))
     f = buf.view(np.float16).astype(np.float64)
     g1 = np.zeros((hid, c))
     g2 = np.zeros((c, hid))
@@ -120,10 +126,9 @@ def test_ffn_pack_roundtrip(c, hid):
                         g1[s * HS + hh, ch] = v
                     else:
                         assert v == 0
-        for kc in range(kc2):
-            for nn in range(c):
-                for k in range(32):
-                    q = at(kc * c16 + nn, k)
-                    g2[nn, s * HS + kc * 32 + k] = f[b + 2 * w1n + q] + f[b + 2 * w1n + w2n + q] / 2048
+        for nn in range(c):
+            for k in range(32):
+                q = at(nn, k)
+                g2[nn, s * HS + perm(k)] = f[b + 2 * w1n + q] + f[b + 2 * w1n + w2n + q] / 2048
     for got, ref in ((g1, w1), (g2, w2)):
         assert np.all(np.abs(got - ref) <= np.abs(ref) * 2.0 ** -21 + 2.0 ** -35)
