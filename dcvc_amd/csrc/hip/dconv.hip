@@ -49,6 +49,7 @@ struct DP {
   const float *res, *res2; // residuals (output views) or NULL
   int rcs, rco, r2cs, r2co;
   int shuffle;             // pixel_shuffle(2) on store (output H, W doubled, channels / 4)
+  int xcd;                 // XCD-aware n-block mapping (grid a multiple of 8 nblk)
   int *ovf;
 };
 
@@ -83,8 +84,16 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
   const int GR = gridDim.x;
   // workgroup -> (output-channel block, first tile): the block is fixed per
   // workgroup, so its weights are loaded once
-  const int nb = blockIdx.x % p.nblk;
-  const int gs = blockIdx.x / p.nblk, GS = GR / p.nblk;
+  int nb = blockIdx.x % p.nblk, gs = blockIdx.x / p.nblk;
+  if (p.xcd) {
+    // workgroups are dealt to the 8 XCDs round robin: the nblk workgroups
+    // that walk the same tiles (one per n-block) on one XCD, so all but the
+    // first read each input pixel from that XCD's L2
+    const int b = blockIdx.x >> 3;
+    nb = b % p.nblk;
+    gs = (blockIdx.x & 7) + 8 * (b / p.nblk);
+  }
+  const int GS = GR / p.nblk;
   if (gs >= GS) return;
   const int n0 = nb * BN;
 
@@ -246,6 +255,21 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
 #pragma unroll
           for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], v[e] * p.slope);
         }
+        if (p.shuffle && p.cout % 16) {
+          // (narrow upsampler, subpel_conv1x1 to 4 x 2 channels: element
+          // stores) conv channel n0 + c + e -> output channel (n0 + c) / 4 of
+          // sub-pixel e
+          const int cc = n0 + c;
+          if (live && cc < p.cout) {
+            const float s = Lc[BN + c / 4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const int ry = 2 * oy + (e >> 1), cx = 2 * ox + (e & 1);
+              p.y[((int64_t)ry * 2 * p.Wo + cx) * p.ycs + p.yco + cc / 4] = v[e] * s;
+            }
+          }
+          continue;
+        }
         if (p.shuffle) {
           // lane row q holds conv channels n0 + 16 n + 4 q + e: a 4 x 4
           // transpose across the rows gives row q the 4 consecutive output
@@ -327,6 +351,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
 int g_cus = 0;
 int g_enable = 1;   // dcvc_set_option("dconv", 0): route these layers to sconv.hip
 int g_k1 = 1;       // dcvc_set_option("dconv_1x1", 0): stride-1 1x1 layers to sgemm.hip
+int g_xcd = 1;      // dcvc_set_option("dconv_xcd", 0): n-blocks of a tile on different XCDs (A/B)
 
 template <int KS, int BN, int NP>
 int launch(DP p, hipStream_t st) {
@@ -352,6 +377,7 @@ int launch(DP p, hipStream_t st) {
   if (per > need) per = need;
   if (per < 1) per = 1;
   const int64_t grid = per * p.nblk;
+  p.xcd = p.nblk > 1 && g_xcd && grid % (8 * p.nblk) == 0;
   auto kern = dconv_kernel<KS, BN, NP>;
   dcvc_note_kernel("dconv_kernel<%d, %d, %d>@%lld", KS, BN, NP, (long long)grid * 512);
   dcvc_ensure_lds(reinterpret_cast<const void *>(kern), 160 * 1024);
@@ -380,6 +406,7 @@ int pick(DP p, hipStream_t st) {
 
 extern "C" void dcvc_internal_dconv_enable(int v) { g_enable = v; }
 extern "C" void dcvc_internal_dconv_1x1(int v) { g_k1 = v; }
+extern "C" void dcvc_internal_dconv_xcd(int v) { g_xcd = v; }
 
 // Stride-2 3x3 / 1x1 and feature-rate 1x1 f16x3 convolutions with fp32
 // views (dcvc_conv2d tries it before sconv.hip).  DCVC_HIP_EUNSUPPORTED:
@@ -393,8 +420,11 @@ extern "C" int dcvc_internal_dconv(const dcvc_conv_args *a, void *stream) {
   // its K loop's load latency shows; sgemm.hip keeps those)
   const bool s2 = a->stride == 2 && (a->kh == 3 || a->kh == 1);
   const bool k1 = a->stride == 1 && a->kh == 1 && g_k1 && (int64_t)a->x.H * a->x.W >= 65536;
+  // (stride-1 3x3 / 7x7 layers with fewer than 16 output channels stay on
+  // sconv.hip: 48 -> 3 3x3 at 1080p 204 us there vs 337 us here, 16 -> 2 7x7
+  // 375 vs 525 us, profiles/r05k_micro.jsonl)
   if (!s2 && !k1) return DCVC_HIP_EUNSUPPORTED;
-  if (a->shuffle && (!k1 || a->cout % 16 || a->res.ptr || a->res2.ptr)) return DCVC_HIP_EUNSUPPORTED;
+  if (a->shuffle && (!k1 || a->cout % 4 || a->res.ptr || a->res2.ptr)) return DCVC_HIP_EUNSUPPORTED;
   if (a->res2.ptr && !a->res.ptr) return DCVC_HIP_EUNSUPPORTED;
   if (a->in_op != DCVC_IN_NONE && !(a->in_op == DCVC_IN_LRELU && a->in_slope >= 0.f && a->in_slope <= 1.f))
     return DCVC_HIP_EUNSUPPORTED;
@@ -407,7 +437,7 @@ extern "C" int dcvc_internal_dconv(const dcvc_conv_args *a, void *stream) {
   };
   if (a->res.ptr && (!vec_ok(a->res) || a->cout % 4)) return DCVC_HIP_EUNSUPPORTED;
   if (a->res2.ptr && !vec_ok(a->res2)) return DCVC_HIP_EUNSUPPORTED;
-  if (a->shuffle && !vec_ok(a->y)) return DCVC_HIP_EUNSUPPORTED;
+  if (a->shuffle && a->cout % 16 == 0 && !vec_ok(a->y)) return DCVC_HIP_EUNSUPPORTED;
   DP p{};
   // outputs: 16-byte pieces of 4 channels where the view allows, else
   // element stores (SpyNet's 2-channel flow)

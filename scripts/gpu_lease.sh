@@ -5,7 +5,7 @@
 #   bench3   the default C3 bench line (3 lanes)
 #   tests    pytest -m gpu   (PYTEST_ARGS: targets / options, default tests)
 #   smoke    __graft_entry__.smoke()
-#   micro    scripts/sconv_bench.py $MICRO_ARGS (kernel microbenchmarks)
+#   micro    scripts/sconv_bench.py $MICRO_ARGS, then $MICRO_ARGS2..4 if set (kernel microbenchmarks)
 #   prof     rocprofv3 kernel stats of a one-lane bench
 #   ab       interleaved A/B of $AB_SHAPES (scripts/sconv_bench.py): the product library, then
 #            dcvc_amd/lib/$AB_LIB (DCVC_HIP_LIB), twice each, one JSON line per shape and arm
@@ -29,8 +29,9 @@ for s in $STEPS; do
               --timeout-method thread > gpurun_out/${TAG}_pytest.log 2>&1 ;;
     smoke)  timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${TAG}_smoke.log 2>&1 ;;
     micro)  { timeout -k 10 300 python -u scripts/sconv_bench.py ${MICRO_ARGS:-} &&
-              if [ -n "${MICRO_ARGS2:-}" ]; then timeout -k 10 300 python -u scripts/sconv_bench.py ${MICRO_ARGS2}; fi; } \
-              > gpurun_out/${TAG}_micro.jsonl 2> gpurun_out/${TAG}_micro.err ;;
+              for m in "${MICRO_ARGS2:-}" "${MICRO_ARGS3:-}" "${MICRO_ARGS4:-}"; do
+                if [ -n "$m" ]; then timeout -k 10 300 python -u scripts/sconv_bench.py $m || exit 1; fi
+              done; } > gpurun_out/${TAG}_micro.jsonl 2> gpurun_out/${TAG}_micro.err ;;
     prof)   timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_prof -o run --output-format csv \
               -- python bench.py --lanes 1 --steps 6 --warmup 2 --no-cpu-baseline --no-roofline \
               > gpurun_out/${TAG}_prof.log 2>&1 ;;

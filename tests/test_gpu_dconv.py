@@ -2,8 +2,9 @@
 
 dconv_kernel takes the stride-2 3x3 / 1x1 layers of the strided encoders
 (DCVC-DC/src/models/video_model.py:66-86, 173-195; ResidualBlockWithStride)
-and the feature-rate 1x1 layers (DepthConv, subpel_conv1x1,
-DCVC-DC/src/models/layers.py:23-34, 135-163).  It computes the same products
+and the feature-rate 1x1 layers (DepthConv, subpel_conv1x1 incl. the
+narrow 64 -> 8 one, DCVC-DC/src/models/layers.py:23-34, 135-163).  It
+computes the same products
 in the same K order (dcvc_conv_pack_weights' chunks, taps packed in a narrow
 last chunk) with the same epilogue as sconv_kernel / sgemm_kernel, so its
 output must be bit-identical to theirs (dcvc_set_option("dconv", 0) routes
@@ -54,10 +55,13 @@ CASES = [
     (128, 64, 1, 1, 272, 250, False, True, 0, False),
     (64, 256, 1, 1, 256, 260, False, False, 0, True),   # subpel_conv1x1: pixel shuffle on store
     (64, 128, 1, 1, 272, 243, False, True, 0, True),
+    # a narrow upsampler (64 -> 8 1x1 + pixel shuffle to 2 channels: element stores)
+    (64, 8, 1, 1, 256, 260, False, False, 0, True),
+    (64, 8, 1, 1, 256, 263, True, True, 0, True),
 ]
 # shapes dconv leaves to sconv / sgemm (more than two output-channel blocks of
 # a 3x3 stride-2 layer; latent-rate 1x1)
-FALLBACK = [(128, 96, 3, 2, 34, 60), (192, 96, 3, 2, 17, 31), (384, 384, 1, 1, 68, 120), (1024, 256, 1, 1, 17, 30)]
+FALLBACK = [(128, 96, 3, 2, 34, 60), (8, 32, 7, 1, 40, 50), (16, 2, 7, 1, 40, 50), (48, 3, 3, 1, 40, 50), (192, 96, 3, 2, 17, 31), (384, 384, 1, 1, 68, 120), (1024, 256, 1, 1, 17, 30)]
 
 
 @pytest.mark.parametrize("case", FALLBACK)
