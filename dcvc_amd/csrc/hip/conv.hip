@@ -592,6 +592,7 @@ extern "C" int dcvc_internal_dconv(const dcvc_conv_args *a, void *stream);
 extern "C" void dcvc_internal_dconv_enable(int v);
 extern "C" void dcvc_internal_dconv_1x1(int v);
 extern "C" void dcvc_internal_dconv_xcd(int v);
+extern "C" void dcvc_internal_dconv_bn128(int v);
 
 // fp16 range guard of the split kernels (split.h SplitRange): one flag per
 // calling host thread (concurrent GOP lanes each launch from their own thread
@@ -824,6 +825,10 @@ extern "C" int dcvc_set_option(const char *name, int value) {
   }
   if (std::strcmp(name, "dconv_xcd") == 0) {
     dcvc_internal_dconv_xcd(value);
+    return DCVC_HIP_OK;
+  }
+  if (std::strcmp(name, "dconv_bn128") == 0) {
+    dcvc_internal_dconv_bn128(value);
     return DCVC_HIP_OK;
   }
   if (std::strcmp(name, "conv3x3_rows4") == 0) {

@@ -242,6 +242,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
     for (int j = 0; j < NP; ++j) {
       const int ox = ox0 + j * 16 + col;
       const bool live = ox < p.Wo;
+      uint32_t sh[4][4];   // (pixel shuffle, NT % 4 == 0) a group of four n
 #pragma unroll
       for (int n = 0; n < NT; ++n) {
         const int c = n * 16 + q * 4;
@@ -276,16 +277,36 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
           // channels (n0 + 16 n) / 4 + e of sub-pixel q (xconv.hip's epilogue)
           uint32_t x0 = __float_as_uint(v[0]), x1 = __float_as_uint(v[1]);
           uint32_t x2 = __float_as_uint(v[2]), x3 = __float_as_uint(v[3]);
-#ifdef __HIP_DEVICE_COMPILE__
-          const auto a02 = __builtin_amdgcn_permlane32_swap(x0, x2, false, false);
-          const auto a13 = __builtin_amdgcn_permlane32_swap(x1, x3, false, false);
-          const auto b01 = __builtin_amdgcn_permlane16_swap(a02[0], a13[0], false, false);
-          const auto b23 = __builtin_amdgcn_permlane16_swap(a02[1], a13[1], false, false);
-          x0 = b01[0];
-          x1 = b01[1];
-          x2 = b23[0];
-          x3 = b23[1];
-#endif
+          xpose4(x0, x1, x2, x3);
+          if constexpr (NT % 4 == 0) {
+            // groups of four n: a second transpose, across (row, n), gives row
+            // q the output channels (n0 + 64 g) / 4 + 4 q .. + 3 of every
+            // sub-pixel, so the 4 rows store 64 contiguous bytes of one
+            // output pixel per instruction (not 16 bytes of 4 pixels)
+            const int g = n >> 2, k = n & 3;
+            sh[k][0] = x0;
+            sh[k][1] = x1;
+            sh[k][2] = x2;
+            sh[k][3] = x3;
+            if (k == 3) {
+#pragma unroll
+              for (int e = 0; e < 4; ++e) xpose4(sh[0][e], sh[1][e], sh[2][e], sh[3][e]);
+              const int cl = 16 * g + 4 * q;   // the lane's 4 channels, relative to n0 / 4
+              const float4 sc = *reinterpret_cast<const float4 *>(Lc + BN + cl);
+#pragma unroll
+              for (int s = 0; s < 4; ++s) {
+                f32x4 o;
+                o[0] = __uint_as_float(sh[s][0]) * sc.x;
+                o[1] = __uint_as_float(sh[s][1]) * sc.y;
+                o[2] = __uint_as_float(sh[s][2]) * sc.z;
+                o[3] = __uint_as_float(sh[s][3]) * sc.w;
+                const int ry = 2 * oy + (s >> 1), cx = 2 * ox + (s & 1);
+                if (live && n0 + 64 * g + 16 * q < p.cout)   // (row q: n = 4 g + q)
+                  *reinterpret_cast<f32x4 *>(p.y + ((int64_t)ry * 2 * p.Wo + cx) * p.ycs + p.yco + (n0 >> 2) + cl) = o;
+              }
+            }
+            continue;
+          }
           const int cb = (n0 >> 2) + 4 * n;   // first output channel of the 16-channel group
           const float4 sc = *reinterpret_cast<const float4 *>(Lc + BN + 4 * n);
           f32x4 o;
@@ -351,6 +372,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
 int g_cus = 0;
 int g_enable = 1;   // dcvc_set_option("dconv", 0): route these layers to sconv.hip
 int g_k1 = 1;       // dcvc_set_option("dconv_1x1", 0): stride-1 1x1 layers to sgemm.hip
+int g_bn128 = 1;   // dcvc_set_option("dconv_bn128", 0): 64-channel n-blocks for 1x1 layers (A/B)
 int g_xcd = 1;      // dcvc_set_option("dconv_xcd", 0): n-blocks of a tile on different XCDs (A/B)
 
 template <int KS, int BN, int NP>
@@ -395,6 +417,11 @@ int pick(DP p, hipStream_t st) {
     return (size_t)p.nst * 2 * bn * 32 * 2 + (size_t)2 * bn * 4 <= 160 * 1024 && (KS == 1 || 2 * bn >= p.cout);
   };
   if (p.cout % 16) return fits(16) ? launch<KS, 16, NP>(p, st) : DCVC_HIP_EUNSUPPORTED;
+  // (1x1 with 128-channel multiples: one 128-row block of one 16-pixel group
+  // per wave reads the input once instead of once per 64-channel block;
+  // 64 -> 128 + shuffle at 544 x 960 110 -> 103 us, 64 -> 256 + shuffle at
+  // 272 x 480 50 -> 47 us, profiles/r05m_dconv_shuffle_bn128_ab.jsonl)
+  if (KS == 1 && g_bn128 && p.cout % 128 == 0 && fits(128)) return launch<KS, 128, 1>(p, st);
   if (p.cout % 64 == 0 && fits(64)) return launch<KS, 64, NP>(p, st);
   if (p.cout % 48 == 0 && fits(48)) return launch<KS, 48, NP>(p, st);
   if (p.cout % 32 == 0 && fits(32)) return launch<KS, 32, NP>(p, st);
@@ -407,6 +434,7 @@ int pick(DP p, hipStream_t st) {
 extern "C" void dcvc_internal_dconv_enable(int v) { g_enable = v; }
 extern "C" void dcvc_internal_dconv_1x1(int v) { g_k1 = v; }
 extern "C" void dcvc_internal_dconv_xcd(int v) { g_xcd = v; }
+extern "C" void dcvc_internal_dconv_bn128(int v) { g_bn128 = v; }
 
 // Stride-2 3x3 / 1x1 and feature-rate 1x1 f16x3 convolutions with fp32
 // views (dcvc_conv2d tries it before sconv.hip).  DCVC_HIP_EUNSUPPORTED:

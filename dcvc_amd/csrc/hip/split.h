@@ -37,6 +37,21 @@ __device__ __forceinline__ uint32_t pk(float a, float b) {
 // (fmaxf would first quieten v, a signalling NaN for all the compiler knows:
 // one more instruction per element); the same value for every non-NaN v,
 // signed zeros included
+// 4 x 4 transpose across the four 16-lane rows of a wave and four registers:
+// row r's x_j <- row j's x_r
+__device__ __forceinline__ void xpose4(uint32_t &x0, uint32_t &x1, uint32_t &x2, uint32_t &x3) {
+#ifdef __HIP_DEVICE_COMPILE__
+  const auto a02 = __builtin_amdgcn_permlane32_swap(x0, x2, false, false);
+  const auto a13 = __builtin_amdgcn_permlane32_swap(x1, x3, false, false);
+  const auto b01 = __builtin_amdgcn_permlane16_swap(a02[0], a13[0], false, false);
+  const auto b23 = __builtin_amdgcn_permlane16_swap(a02[1], a13[1], false, false);
+  x0 = b01[0];
+  x1 = b01[1];
+  x2 = b23[0];
+  x3 = b23[1];
+#endif
+}
+
 __device__ __forceinline__ float lrelu_in(float v, float s) {
   const float t = v * s;
 #ifdef __HIP_DEVICE_COMPILE__

@@ -553,39 +553,64 @@ xconv3_kernel(XP p) {
       // holds conv channels n0 + 16 j + 4 hi + e (e = 2 dy + dx): a 4 x 4
       // transpose across the rows (v_permlane32_swap, then v_permlane16_swap)
       // gives row hi the 4 consecutive output channels (n0 + 16 j) / 4 + e of
-      // sub-pixel hi, one 16-byte store; then the output-channel scale
+      // sub-pixel hi; then the output-channel scale
       const __amdgpu_buffer_rsrc_t ys = __builtin_amdgcn_make_buffer_rsrc(
           p.y + (int64_t)(2 * ti.oy0) * (2 * p.Wo) * p.ycs + p.yco, (short)0, 0x7fff0000, 0x00020000);
 #pragma unroll
-      for (int r = 0; r < RW; ++r)
+      for (int r = 0; r < RW; ++r) {
+        uint32_t sh[4][4];   // a group of four j (NT % 4 == 0)
 #pragma unroll
         for (int j = 0; j < NT; ++j) {
           // (__float_as_uint: hipcc's __builtin_bit_cast of a vector element
           // reads element 0 whatever the index)
           uint32_t x0 = __float_as_uint(v[r][j][0]), x1 = __float_as_uint(v[r][j][1]);
           uint32_t x2 = __float_as_uint(v[r][j][2]), x3 = __float_as_uint(v[r][j][3]);
-#ifdef __HIP_DEVICE_COMPILE__
-          const auto a02 = __builtin_amdgcn_permlane32_swap(x0, x2, false, false);
-          const auto a13 = __builtin_amdgcn_permlane32_swap(x1, x3, false, false);
-          const auto b01 = __builtin_amdgcn_permlane16_swap(a02[0], a13[0], false, false);
-          const auto b23 = __builtin_amdgcn_permlane16_swap(a02[1], a13[1], false, false);
-          x0 = b01[0];
-          x1 = b01[1];
-          x2 = b23[0];
-          x3 = b23[1];
-#endif
-          const int cb = (ti.n0 >> 2) + 4 * j;
-          const float4 sc = *reinterpret_cast<const float4 *>(Lc + p.cout + cb);
-          f32x4 o;
-          o[0] = __uint_as_float(x0) * sc.x;
-          o[1] = __uint_as_float(x1) * sc.y;
-          o[2] = __uint_as_float(x2) * sc.z;
-          o[3] = __uint_as_float(x3) * sc.w;
-          const int ry = 2 * (wave * RW + r) + (hi >> 1), cx = 2 * (ti.ox0 + col) + (hi & 1);
-          const bool ok = ti.oy0 + wave * RW + r < p.Ho && ti.ox0 + col < p.Wo && ti.n0 + 16 * j < p.cout;
-          const int off = ok ? ((ry * 2 * p.Wo + cx) * p.ycs + cb) * 4 : 0x7ffffff0;
-          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, o), ys, off, 0, 0);
+          xpose4(x0, x1, x2, x3);
+          const int ry0 = 2 * (wave * RW + r), cx0 = 2 * (ti.ox0 + col);
+          const bool okp = ti.oy0 + wave * RW + r < p.Ho && ti.ox0 + col < p.Wo;
+          if constexpr (NT % 4 == 0) {
+            // groups of four j: a second transpose, across (row, j), gives
+            // row hi the output channels (n0 + 64 g) / 4 + 4 hi .. + 3 of
+            // every sub-pixel, so the 4 rows store 64 contiguous bytes of one
+            // output pixel per instruction (not 16 bytes of 4 pixels)
+            const int g = j >> 2, k = j & 3;
+            sh[k][0] = x0;
+            sh[k][1] = x1;
+            sh[k][2] = x2;
+            sh[k][3] = x3;
+            if (k == 3) {
+#pragma unroll
+              for (int e = 0; e < 4; ++e) xpose4(sh[0][e], sh[1][e], sh[2][e], sh[3][e]);
+              const int cb = (ti.n0 >> 2) + 16 * g + 4 * hi;
+              const float4 sc = *reinterpret_cast<const float4 *>(Lc + p.cout + cb);
+              const bool ok = okp && ti.n0 + 64 * g + 16 * hi < p.cout;   // (row hi: conv block j = 4 g + hi)
+#pragma unroll
+              for (int s = 0; s < 4; ++s) {
+                f32x4 o;
+                o[0] = __uint_as_float(sh[s][0]) * sc.x;
+                o[1] = __uint_as_float(sh[s][1]) * sc.y;
+                o[2] = __uint_as_float(sh[s][2]) * sc.z;
+                o[3] = __uint_as_float(sh[s][3]) * sc.w;
+                const int ry = ry0 + (s >> 1), cx = cx0 + (s & 1);
+                const int off = ok ? ((ry * 2 * p.Wo + cx) * p.ycs + cb) * 4 : 0x7ffffff0;
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, o), ys, off, 0, 0);
+              }
+            }
+          } else {
+            const int cb = (ti.n0 >> 2) + 4 * j;
+            const float4 sc = *reinterpret_cast<const float4 *>(Lc + p.cout + cb);
+            f32x4 o;
+            o[0] = __uint_as_float(x0) * sc.x;
+            o[1] = __uint_as_float(x1) * sc.y;
+            o[2] = __uint_as_float(x2) * sc.z;
+            o[3] = __uint_as_float(x3) * sc.w;
+            const int ry = ry0 + (hi >> 1), cx = cx0 + (hi & 1);
+            const bool ok = okp && ti.n0 + 16 * j < p.cout;
+            const int off = ok ? ((ry * 2 * p.Wo + cx) * p.ycs + cb) * 4 : 0x7ffffff0;
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, o), ys, off, 0, 0);
+          }
         }
+      }
       return;
     }
     if constexpr (NRES >= 1) {

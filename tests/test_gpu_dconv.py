@@ -145,3 +145,35 @@ def test_dconv_repeatable_and_interleaved():
         h.conv(cw, x, y0)
     torch.cuda.synchronize()
     assert torch.equal(y0.buf, ref)
+
+
+@pytest.mark.parametrize("case", [(128, 128, 272, 241, False), (64, 256, 256, 260, True), (128, 256, 40, 70, True)])
+def test_dconv_bn128_matches_sgemm(case):
+    """1x1 layers with 128-channel n-blocks of 16-pixel groups (the default)
+    and with 64-channel blocks of 32 pixels (dcvc_set_option("dconv_bn128",
+    0)): the same bits as sgemm.hip, with and without the pixel shuffle's
+    coalesced store."""
+    h = K()
+    cin, cout, H, W, shuf = case
+    g = torch.Generator().manual_seed(cin + cout + H)
+    x = h.from_nchw(torch.randn(1, cin, H, W, generator=g), h.F32)
+    cw = h.ConvW(torch.randn(cout, cin, 1, 1, generator=g) / cin ** 0.5, torch.randn(cout, generator=g) * 0.1, 1,
+                 h.F16X3)
+    sc = (torch.rand(cout // 4 if shuf else cout, generator=g) + 0.5).cuda()
+    outs = []
+    for opts in ({"dconv_bn128": 1}, {"dconv_bn128": 0}, {"dconv": 0}):
+        for k, v in opts.items():
+            h.set_option(k, v)
+        try:
+            y = h.conv(cw, x, out_dtype=h.F32, scale=sc, shuffle=shuf, act=h.ACT_LRELU, slope=0.1)
+            torch.cuda.synchronize()
+            kern = h.lib().dcvc_last_kernel().decode()
+        finally:
+            h.set_option("dconv_bn128", 1)
+            h.set_option("dconv", 1)
+        outs.append((kern, y.buf.cpu()))
+    big = H * W >= 65536
+    assert outs[0][0].startswith("dconv_kernel<1, 128, 1>" if big else ("sgemm_kernel", "sconv_kernel")), outs[0][0]
+    assert outs[1][0].startswith("dconv_kernel<1, 64, 2>" if big else ("sgemm_kernel", "sconv_kernel")), outs[1][0]
+    assert outs[2][0].startswith(("sgemm_kernel", "sconv_kernel")), outs[2][0]
+    assert torch.equal(outs[0][1], outs[2][1]) and torch.equal(outs[1][1], outs[2][1])
