@@ -253,36 +253,58 @@ __global__ void __launch_bounds__(kNT) sdc_kernel(DP p) {
     wait_lgkm();
     raw_barrier();
 
-    // ---- P2: d = dw3x3(t1) + bdw, split into D: thread task = (interior
-    // pixel, 4 channels); taps in (dy, dx) order, then the bias
+    // ---- P2: d = dw3x3(t1) + bdw, split into D.  Thread task = (4-channel
+    // group, column, run of RR output rows): a 3 x 3 window of t1 pieces
+    // slides down the run (3 LDS reads per output row, not 9) and the group's
+    // 9 tap weights stay in registers for the run; per output the taps in
+    // (dy, dx) order, then the bias
     {
       constexpr int CG = CIN / 4;
-      for (int it = tid; it < TH * TW * CG; it += kNT) {
-        const int px = it / CG, cg = it - px * CG;
+      constexpr int R = kNT / (CG * TW) >= 4 ? 4 : kNT / (CG * TW) >= 2 ? 2 : 1;   // runs per column
+      constexpr int RR = TH / R;
+      static_assert(CG * TW * R <= kNT && TH % R == 0, "P2 tasks");
+      if (tid < CG * TW * R) {
+        const int cg = tid % CG, rest = tid / CG;
+        const int ix = rest % TW, y0 = (rest / TW) * RR;
         const int c = cg * 4;
-        const int iy = px / TW, ix = px - iy * TW;
-        f32x4 a = f32x4{0.f, 0.f, 0.f, 0.f};
+        f32x4 wv[9];
 #pragma unroll
-        for (int dy = 0; dy < 3; ++dy)
+        for (int k = 0; k < 9; ++k) wv[k] = *reinterpret_cast<const f32x4 *>(Lwdw + k * CIN + c);
+        const float4 bd = *reinterpret_cast<const float4 *>(Lbdw + c);
+        f32x4 win[3][3];   // [halo row mod 3][dx]
 #pragma unroll
-          for (int dx = 0; dx < 3; ++dx) {
-            const f32x4 tv = *reinterpret_cast<const f32x4 *>(t1p((iy + dy) * HW_ + ix + dx, c));
-            const f32x4 wv = *reinterpret_cast<const f32x4 *>(Lwdw + (dy * 3 + dx) * CIN + c);
+        for (int r = 0; r < 2; ++r)
 #pragma unroll
-            for (int e = 0; e < 4; ++e) a[e] = __builtin_fmaf(wv[e], tv[e], a[e]);
-          }
-        float v[4];
+          for (int dx = 0; dx < 3; ++dx)
+            win[r][dx] = *reinterpret_cast<const f32x4 *>(t1p((y0 + r) * HW_ + ix + dx, c));
 #pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = a[e] + Lbdw[c + e];
-        rg.add4(v);
-        const auto h01 = __builtin_amdgcn_cvt_pkrtz(v[0], v[1]);
-        const auto h23 = __builtin_amdgcn_cvt_pkrtz(v[2], v[3]);
-        const uint32_t l01 = pk(split_lo(v[0], (float)h01[0]), split_lo(v[1], (float)h01[1]));
-        const uint32_t l23 = pk(split_lo(v[2], (float)h23[0]), split_lo(v[3], (float)h23[1]));
-        const int o = swz((c >> 5) * (TH * TW) + px, (c & 31) >> 3) + (c & 7);
-        typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
-        *reinterpret_cast<u32x2_t *>(Dh + o) = u32x2_t{__builtin_bit_cast(uint32_t, h01), __builtin_bit_cast(uint32_t, h23)};
-        *reinterpret_cast<u32x2_t *>(Dl + o) = u32x2_t{l01, l23};
+        for (int i = 0; i < RR; ++i) {
+#pragma unroll
+          for (int dx = 0; dx < 3; ++dx)
+            win[(i + 2) % 3][dx] = *reinterpret_cast<const f32x4 *>(t1p((y0 + i + 2) * HW_ + ix + dx, c));
+          f32x4 a = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+            for (int dx = 0; dx < 3; ++dx)
+#pragma unroll
+              for (int e = 0; e < 4; ++e) a[e] = __builtin_fmaf(wv[dy * 3 + dx][e], win[(i + dy) % 3][dx][e], a[e]);
+          float v[4];
+          v[0] = a[0] + bd.x;
+          v[1] = a[1] + bd.y;
+          v[2] = a[2] + bd.z;
+          v[3] = a[3] + bd.w;
+          rg.add4(v);
+          const auto h01 = __builtin_amdgcn_cvt_pkrtz(v[0], v[1]);
+          const auto h23 = __builtin_amdgcn_cvt_pkrtz(v[2], v[3]);
+          const uint32_t l01 = pk(split_lo(v[0], (float)h01[0]), split_lo(v[1], (float)h01[1]));
+          const uint32_t l23 = pk(split_lo(v[2], (float)h23[0]), split_lo(v[3], (float)h23[1]));
+          const int px = (y0 + i) * TW + ix;
+          const int o = swz((c >> 5) * (TH * TW) + px, (c & 31) >> 3) + (c & 7);
+          typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
+          *reinterpret_cast<u32x2_t *>(Dh + o) = u32x2_t{__builtin_bit_cast(uint32_t, h01), __builtin_bit_cast(uint32_t, h23)};
+          *reinterpret_cast<u32x2_t *>(Dl + o) = u32x2_t{l01, l23};
+        }
       }
       if constexpr (CIN % 32 != 0) {   // D's padding channels: zero
         constexpr int PADQ = KCI * 4 - CIN / 8;

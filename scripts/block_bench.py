@@ -32,6 +32,8 @@ def main():
     torch.manual_seed(0)
     for o in a.opt:
         name, val = o.split("=")
+        if name == "arm":          # A/B label (scripts/gpu_lease.sh ab)
+            continue
         if name == "od_planar":
             K.OD_PLANAR = bool(int(val))
         else:

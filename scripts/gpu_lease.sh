@@ -7,7 +7,7 @@
 #   smoke    __graft_entry__.smoke()
 #   micro    scripts/sconv_bench.py $MICRO_ARGS, then $MICRO_ARGS2..4 if set (kernel microbenchmarks)
 #   prof     rocprofv3 kernel stats of a one-lane bench
-#   ab       interleaved A/B of $AB_SHAPES (scripts/sconv_bench.py): the product library, then
+#   ab       interleaved A/B of $AB_SHAPES (scripts/$AB_TOOL, default sconv_bench.py): the product library, then
 #            dcvc_amd/lib/$AB_LIB (DCVC_HIP_LIB), twice each, one JSON line per shape and arm
 #   bench1b  bench1 with DCVC_HIP_LIB=$AB_LIB
 #   block    scripts/block_bench.py $BLOCK_ARGS (fused blocks / gathers), repeated for $BLOCK_ARGS2 if set
@@ -42,8 +42,8 @@ for s in $STEPS; do
               -- python ${KSTATS_CMD} > gpurun_out/${TAG}_kstats.log 2>&1 ;;
     pmc)    bash scripts/pmc_cmd.sh gpurun_out/${TAG}_pmc python ${PMC_CMD} > gpurun_out/${TAG}_pmc.log 2>&1 ;;
     ab)     { for rep in 1 2; do
-                timeout -k 10 300 python -u scripts/sconv_bench.py --shapes ${AB_SHAPES} --opt arm=A || exit 1
-                DCVC_HIP_LIB=${AB_LIB} timeout -k 10 300 python -u scripts/sconv_bench.py --shapes ${AB_SHAPES} --opt arm=B || exit 1
+                timeout -k 10 300 python -u scripts/${AB_TOOL:-sconv_bench.py} --shapes ${AB_SHAPES} --opt arm=A || exit 1
+                DCVC_HIP_LIB=${AB_LIB} timeout -k 10 300 python -u scripts/${AB_TOOL:-sconv_bench.py} --shapes ${AB_SHAPES} --opt arm=B || exit 1
               done; } > gpurun_out/${TAG}_ab.jsonl 2> gpurun_out/${TAG}_ab.err ;;
     bench1b) DCVC_HIP_LIB=${AB_LIB} timeout -k 10 600 python bench.py --lanes 1 --steps 12 --warmup 3 --no-cpu-baseline \
               --profile-out gpurun_out/${TAG}_layers_b.json ${BENCH_ARGS:-} > gpurun_out/${TAG}_bench1b.log 2>&1 ;;

@@ -412,4 +412,13 @@ def test_fused_depthconv_matches_fp64(cin, cout, adapt, H, W):
     y = h.depth_conv_split(dw, xa, out.ch(8, cout), slope=0.01)
     torch.cuda.synchronize()
     assert y is not None and h.lib().dcvc_last_kernel().decode().startswith("sdc_kernel")
-    assert rel_err(out.ch(8, cout).nchw().cpu(), ref) < TOL
+    got = out.ch(8, cout).nchw().cpu()
+    assert rel_err(got, ref) < TOL
+    # the unfused launches (split 1x1 with the LeakyReLU epilogue, the fp32
+    # depthwise kernel, split 1x1 + identity / adaptor): the same bits
+    t1 = h.conv(h.ConvW(w1, b1, 1, h.F16X3), xa, act=h.ACT_LRELU, slope=0.01)
+    d = h.dwconv3x3(t1, w9c.cuda(), bd.cuda())
+    idn = h.conv(h.ConvW(wa, ba, 1, h.F16X3), xa) if adapt else xa
+    y2 = h.conv(h.ConvW(w2, b2, 1, h.F16X3), d, res=idn)
+    torch.cuda.synchronize()
+    assert torch.equal(y2.nchw().cpu(), got)
