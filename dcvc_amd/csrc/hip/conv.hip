@@ -589,6 +589,8 @@ extern "C" int dcvc_internal_set_option_split(const char *name, int value);
 extern "C" int dcvc_internal_xconv(const dcvc_conv_args *a, void *stream);
 extern "C" void dcvc_internal_xconv_enable(int v);
 extern "C" int dcvc_internal_dconv(const dcvc_conv_args *a, void *stream);
+extern "C" int dcvc_internal_tconv(const dcvc_conv_args *a, void *stream);
+extern "C" void dcvc_internal_tconv_enable(int v);
 extern "C" void dcvc_internal_dconv_enable(int v);
 extern "C" void dcvc_internal_dconv_1x1(int v);
 extern "C" void dcvc_internal_dconv_xcd(int v);
@@ -658,9 +660,11 @@ extern "C" int dcvc_conv2d(const dcvc_conv_args *a, void *stream) {
     p.r2co = a->res2.coff;
   }
   if (a->compute == DCVC_F16X3) {   // the split-fp16 kernels only
-    int r = dcvc_internal_xconv(a, stream);   // static-shape 3x3 stride-1 kernel (xconv.hip)
+    int r = dcvc_internal_tconv(a, stream);   // 2-channel input / <= 4-channel output: fp32 VALU (tconv.hip)
     if (r != DCVC_HIP_EUNSUPPORTED) return r;
-    r = dcvc_internal_dconv(a, stream);       // stride 2 and narrow 7x7: direct operand loads (dconv.hip)
+    r = dcvc_internal_xconv(a, stream);       // static-shape 3x3 stride-1 kernel (xconv.hip)
+    if (r != DCVC_HIP_EUNSUPPORTED) return r;
+    r = dcvc_internal_dconv(a, stream);       // stride 2, feature-rate 1x1: direct operand loads (dconv.hip)
     if (r != DCVC_HIP_EUNSUPPORTED) return r;
     return dcvc_internal_sconv(a, stream);
   }
@@ -821,6 +825,10 @@ extern "C" int dcvc_set_option(const char *name, int value) {
   }
   if (std::strcmp(name, "dconv_1x1") == 0) {
     dcvc_internal_dconv_1x1(value);
+    return DCVC_HIP_OK;
+  }
+  if (std::strcmp(name, "tconv") == 0) {
+    dcvc_internal_tconv_enable(value);
     return DCVC_HIP_OK;
   }
   if (std::strcmp(name, "dconv_xcd") == 0) {

@@ -570,8 +570,12 @@ int launch(SP p, hipStream_t st) {
   // a workgroup keeps one n-block (resident weights, loaded once): the grid
   // stride must be a multiple of the n-block count.  A grid smaller than the
   // n-block count (few CUs, or the sconv_occupancy option) cannot keep that:
-  // the caller then takes the streamed-weight kernel
-  if (RES && G < p.nblk) return DCVC_HIP_EUNSUPPORTED;
+  // the caller then takes the streamed-weight kernel, or for a 1x1 layer
+  // (no streamed variant) the grid grows to one workgroup per n-block
+  if (RES && G < p.nblk) {
+    if (KS != 1) return DCVC_HIP_EUNSUPPORTED;
+    G = p.nblk;
+  }
   if (RES && G % p.nblk) G = G / p.nblk * p.nblk;
   if (G < 1) G = 1;
   auto kern = sconv_kernel<KS, S, BN, RW, NW, GATE, RES>;
@@ -671,7 +675,7 @@ int pick_bn(SP p, hipStream_t st) {
     }
   }
   if constexpr (KS == 1) {
-    return DCVC_HIP_EUNSUPPORTED;   // (a 1x1 n-block of 16 channels always fits resident)
+    return DCVC_HIP_EUNSUPPORTED;   // (a 1x1 n-block of 16 channels always fits resident, at any grid)
   } else {
     // streamed weights; 7x7 layers stay <= 32 channels per n-block
     bn_order(p.cout, KS == 7 ? 32 : 64, order);

@@ -1003,9 +1003,13 @@ extern "C" int dcvc_internal_xconv(const dcvc_conv_args *a, void *stream) {
   }
   if (p.has_res2 && !p.has_res) return DCVC_HIP_EUNSUPPORTED;
   if (!ok) return DCVC_HIP_EUNSUPPORTED;
-  // per-tile buffer offsets stay below 2^31 bytes
+  // per-tile buffer offsets stay below 2^31 bytes: output / residual rows of
+  // a tile (16 rows; with the pixel shuffle 32 rows of 2 Wo pixels) and the
+  // input halo rows (16 + 6 at most)
   if ((int64_t)16 * p.Wo * std::max(p.ycs, std::max(p.rcs, p.r2cs)) * 4 >= ((int64_t)1 << 30))
     return DCVC_HIP_EUNSUPPORTED;
+  if (a->shuffle && (int64_t)32 * 2 * p.Wo * p.ycs * 4 >= ((int64_t)1 << 31) - 64) return DCVC_HIP_EUNSUPPORTED;
+  if ((int64_t)(16 + a->kh) * p.W * p.xcs * 4 >= ((int64_t)1 << 31) - 64) return DCVC_HIP_EUNSUPPORTED;
   const int nch = (a->cin + 31) / 32;
   const int vc = a->cin - 32 * (nch - 1);
   const int tpkl = vc <= 8 ? 4 : vc <= 16 ? 2 : 1;

@@ -61,7 +61,7 @@ CASES = [
 ]
 # shapes dconv leaves to sconv / sgemm (more than two output-channel blocks of
 # a 3x3 stride-2 layer; latent-rate 1x1)
-FALLBACK = [(128, 96, 3, 2, 34, 60), (8, 32, 7, 1, 40, 50), (16, 2, 7, 1, 40, 50), (48, 3, 3, 1, 40, 50), (192, 96, 3, 2, 17, 31), (384, 384, 1, 1, 68, 120), (1024, 256, 1, 1, 17, 30)]
+FALLBACK = [(128, 96, 3, 2, 34, 60), (8, 32, 7, 1, 40, 50), (192, 96, 3, 2, 17, 31), (384, 384, 1, 1, 68, 120), (1024, 256, 1, 1, 17, 30)]
 
 
 @pytest.mark.parametrize("case", FALLBACK)

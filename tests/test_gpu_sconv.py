@@ -30,9 +30,11 @@ def _gpu():
     from dcvc_amd import hip
     hip.set_option("xconv", 0)
     hip.set_option("dconv", 0)
+    hip.set_option("tconv", 0)
     yield
     hip.set_option("xconv", 1)
     hip.set_option("dconv", 1)
+    hip.set_option("tconv", 1)
 
 
 def K():
