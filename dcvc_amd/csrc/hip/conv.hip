@@ -591,6 +591,7 @@ extern "C" void dcvc_internal_xconv_enable(int v);
 extern "C" int dcvc_internal_dconv(const dcvc_conv_args *a, void *stream);
 extern "C" int dcvc_internal_tconv(const dcvc_conv_args *a, void *stream);
 extern "C" void dcvc_internal_tconv_enable(int v);
+extern "C" void dcvc_internal_sffn128(int v);
 extern "C" void dcvc_internal_dconv_enable(int v);
 extern "C" void dcvc_internal_dconv_1x1(int v);
 extern "C" void dcvc_internal_dconv_xcd(int v);
@@ -825,6 +826,10 @@ extern "C" int dcvc_set_option(const char *name, int value) {
   }
   if (std::strcmp(name, "dconv_1x1") == 0) {
     dcvc_internal_dconv_1x1(value);
+    return DCVC_HIP_OK;
+  }
+  if (std::strcmp(name, "sffn128") == 0) {
+    dcvc_internal_sffn128(value);
     return DCVC_HIP_OK;
   }
   if (std::strcmp(name, "tconv") == 0) {

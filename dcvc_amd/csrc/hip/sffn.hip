@@ -322,6 +322,7 @@ sffn_kernel(FP p) {
 }
 
 int g_cus = 0;
+int g_c128 = 1;   // dcvc_set_option("sffn128", 0): C = 128 feature maps on 4 waves of two pixel tiles (A/B)
 
 template <int C, int NW, int NP, int NBUF>
 int run(FP p, hipStream_t st) {
@@ -400,6 +401,8 @@ extern "C" int64_t dcvc_ffn_pack_weights(const float *w1, const float *w2, int c
   return slice * ns;
 }
 
+extern "C" void dcvc_internal_sffn128(int v) { g_c128 = v; }
+
 extern "C" int dcvc_conv_ffn(const dcvc_ffn_args *a, void *stream) {
   if (!a || !a->x.ptr || !a->y.ptr || !a->w || !a->b1 || !a->b2) return DCVC_HIP_EINVAL;
   if (a->x.dtype != DCVC_F32 || a->y.dtype != DCVC_F32 || a->x.C != a->c || a->y.C != a->c ||
@@ -433,15 +436,22 @@ extern "C" int dcvc_conv_ffn(const dcvc_ffn_args *a, void *stream) {
   if ((int64_t)p.npix * p.xcs * 4 >= ((int64_t)1 << 31) - 64) return DCVC_HIP_EUNSUPPORTED;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   // 8 waves (two per SIMD) of two 16-pixel tiles with every slice resident
-  // (C <= 64); C = 128 streams its 16 slices through four 32 KiB buffers to
-  // 4 waves of 512 registers (one per SIMD), with one pixel tile per wave
-  // where two would leave CUs idle (the 68 x 120 latent-rate blocks)
+  // (C <= 64); C = 128 streams its 16 slices through four 32 KiB buffers, to
+  // 8 waves of one pixel tile on feature maps, and to 4 waves of 512
+  // registers (one per SIMD) of one tile where more waves would leave CUs
+  // idle (the 68 x 120 latent-rate blocks)
   const int ntiles2 = (p.npix + 4 * 2 * 16 - 1) / (4 * 2 * 16);
   switch (a->c) {
     case 32: return run<32, 8, 2, 0>(p, st);
     case 48: return run<48, 8, 2, 0>(p, st);
     case 64: return run<64, 8, 2, 0>(p, st);
-    case 128: return ntiles2 >= 2 * 256 ? run<128, 4, 2, 4>(p, st) : run<128, 4, 1, 4>(p, st);
+    case 128:
+      // feature maps: 8 waves (two per SIMD, 232 VGPRs, no AGPR copies) of one
+      // pixel tile: 128 -> 512 -> 128 at 272 x 480 154 -> 126 us against 4
+      // waves of two tiles (256 VGPRs + 231 AGPRs, accumulators copied
+      // between the files), profiles/r05t_ffn128_ab.jsonl
+      if (ntiles2 < 2 * 256) return run<128, 4, 1, 4>(p, st);
+      return g_c128 ? run<128, 8, 1, 4>(p, st) : run<128, 4, 2, 4>(p, st);
     default: return DCVC_HIP_EUNSUPPORTED;
   }
 }

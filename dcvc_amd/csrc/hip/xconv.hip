@@ -851,6 +851,7 @@ int g_enable = 1;   // dcvc_set_option("xconv", 0): route every split conv to sc
 // publish, 32 no image-operand reads, 64 no image loads, 128 no residual loads
 // and output stores
 int g_dbg = 0;
+int g_rw1 = 0;
 
 template <int CIN, int BN, int RW, int NW, int NRES, bool SHUF = false, int KS = 3>
 int launch(XP p, hipStream_t st) {
@@ -910,6 +911,12 @@ int pick_bn(XP p, hipStream_t st) {
     if (p.cout % 48 == 0) return launch<CIN, 48, 2, 8, 0, true>(p, st);
     return launch<CIN, 32, 2, 8, 0, true>(p, st);
   }
+  if constexpr (CIN == 64 || CIN == 128) {
+    // residual layers of 64-channel multiples: 8-row tiles (one row per wave)
+    // of 64-channel blocks instead of 16-row tiles of 32-channel blocks, which
+    // load and split the input once per block (A/B: "xconv_rw1")
+    if (g_rw1 && p.has_res && p.cout % 64 == 0) return pick_res<CIN, 64, 1, 8, RES_OK>(p, st);
+  }
   if (p.cout == 32 || p.cout == 48) return p.cout == 32 ? pick_res<CIN, 32, 2, 8, RES_OK>(p, st) : pick_res<CIN, 48, 2, 8, RES_OK>(p, st);
   if (p.cout % 64 == 0 && !p.has_res) return launch<CIN, 64, 2, 8, 0>(p, st);
   if (p.cout % 48 == 0) return pick_res<CIN, 48, 2, 8, RES_OK>(p, st);
@@ -939,6 +946,7 @@ extern "C" int dcvc_internal_set_option_split(const char *name, int value) {
   if (std::strcmp(name, "sconv_dbg") == 0) dcvc_internal_sconv_dbg(value);
   else if (std::strcmp(name, "sconv_rw") == 0) dcvc_internal_sconv_rw(value);
   else if (std::strcmp(name, "xconv_dbg") == 0) g_dbg = value;
+  else if (std::strcmp(name, "xconv_rw1") == 0) g_rw1 = value;
   else return DCVC_HIP_EINVAL;
   return DCVC_HIP_OK;
 }

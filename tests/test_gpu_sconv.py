@@ -287,7 +287,7 @@ def test_sconv_fp16_subnormal_operands():
     assert rel_err(y.nchw().cpu(), ref) < 1e-4
 
 
-@pytest.mark.parametrize("c,H,W", [(48, 37, 53), (32, 20, 70), (64, 33, 31), (128, 17, 30)])
+@pytest.mark.parametrize("c,H,W", [(48, 37, 53), (32, 20, 70), (64, 33, 31), (128, 17, 30), (128, 200, 331)])
 def test_fused_ffn_matches_fp64(c, H, W):
     """sffn.hip: out = scale * (x + lrelu(ffn2(lrelu(ffn1(x) + b1)) + b2))
     (ConvFFN, DCVC-DC/src/models/layers.py:166-179) in one kernel, on channel
@@ -311,7 +311,21 @@ def test_fused_ffn_matches_fp64(c, H, W):
     y = h.conv_ffn(fw, xa, out.ch(4, c), scale=sc.cuda(), slope=0.1)
     torch.cuda.synchronize()
     assert y is not None and h.lib().dcvc_last_kernel().decode().startswith("sffn_kernel")
-    assert rel_err(out.ch(4, c).nchw().cpu(), ref) < TOL
+    got = out.ch(4, c).nchw().cpu()
+    assert rel_err(got, ref) < TOL
+    if c == 128 and H * W >= 512 * 128:
+        # feature maps: 8 waves of one pixel tile (the default) and 4 waves of
+        # two (dcvc_set_option("sffn128", 0)): the same products in the same
+        # order, the same bits
+        assert h.lib().dcvc_last_kernel().decode().startswith("sffn_kernel<128, 8, 1, 4>")
+        h.set_option("sffn128", 0)
+        try:
+            h.conv_ffn(fw, xa, out.ch(4, c), scale=sc.cuda(), slope=0.1)
+            torch.cuda.synchronize()
+            assert h.lib().dcvc_last_kernel().decode().startswith("sffn_kernel<128, 4, 2, 4>")
+        finally:
+            h.set_option("sffn128", 1)
+        assert torch.equal(out.ch(4, c).nchw().cpu(), got)
 
 
 @pytest.mark.parametrize("c,H,W", [(384, 68, 120), (192, 68, 120), (384, 17, 30), (192, 5, 7), (384, 3, 11)])

@@ -193,7 +193,8 @@ def test_shared_pool_concurrent_coders_byte_exact():
     ct = P.CdfTable(*tab)
     base = _nthreads()
     coders = [(P.RansEncoder(True, 8), P.RansDecoder(8)) for _ in range(12)]
-    assert _nthreads() == base, "coders must not start threads of their own"
+    # (<=: a thread another test left behind may end meanwhile)
+    assert _nthreads() <= base, "coders must not start threads of their own"
     jobs = []
     for k in range(6):
         s, i = symbols(20000 + 977 * k, tab[0].shape[0], 100 + k, wide=(k % 3 == 0))
@@ -220,4 +221,4 @@ def test_shared_pool_concurrent_coders_byte_exact():
     for t in th:
         t.join()
     assert not errors, errors
-    assert _nthreads() == base
+    assert _nthreads() <= base
