@@ -591,6 +591,8 @@ extern "C" void dcvc_internal_xconv_enable(int v);
 extern "C" int dcvc_internal_dconv(const dcvc_conv_args *a, void *stream);
 extern "C" int dcvc_internal_tconv(const dcvc_conv_args *a, void *stream);
 extern "C" void dcvc_internal_tconv_enable(int v);
+extern "C" int dcvc_internal_nconv(const dcvc_conv_args *a, void *stream);
+extern "C" void dcvc_internal_nconv_enable(int v);
 extern "C" void dcvc_internal_sffn128(int v);
 extern "C" void dcvc_internal_dconv_enable(int v);
 extern "C" void dcvc_internal_dconv_1x1(int v);
@@ -661,7 +663,9 @@ extern "C" int dcvc_conv2d(const dcvc_conv_args *a, void *stream) {
     p.r2co = a->res2.coff;
   }
   if (a->compute == DCVC_F16X3) {   // the split-fp16 kernels only
-    int r = dcvc_internal_tconv(a, stream);   // 2-channel input / <= 4-channel output: fp32 VALU (tconv.hip)
+    int r = dcvc_internal_tconv(a, stream);   // 2-channel inputs: fp32 VALU (tconv.hip)
+    if (r != DCVC_HIP_EUNSUPPORTED) return r;
+    r = dcvc_internal_nconv(a, stream);       // 2- / 3-channel outputs: pixels on M (nconv.hip)
     if (r != DCVC_HIP_EUNSUPPORTED) return r;
     r = dcvc_internal_xconv(a, stream);       // static-shape 3x3 stride-1 kernel (xconv.hip)
     if (r != DCVC_HIP_EUNSUPPORTED) return r;
@@ -830,6 +834,10 @@ extern "C" int dcvc_set_option(const char *name, int value) {
   }
   if (std::strcmp(name, "sffn128") == 0) {
     dcvc_internal_sffn128(value);
+    return DCVC_HIP_OK;
+  }
+  if (std::strcmp(name, "nconv") == 0) {
+    dcvc_internal_nconv_enable(value);
     return DCVC_HIP_OK;
   }
   if (std::strcmp(name, "tconv") == 0) {

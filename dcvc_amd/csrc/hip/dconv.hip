@@ -451,6 +451,8 @@ extern "C" int dcvc_internal_dconv(const dcvc_conv_args *a, void *stream) {
   // (stride-1 3x3 / 7x7 layers with fewer than 16 output channels stay on
   // sconv.hip: 48 -> 3 3x3 at 1080p 204 us there vs 337 us here, 16 -> 2 7x7
   // 375 vs 525 us, profiles/r05k_micro.jsonl)
+  // (SpyNet's first 7x7, 8 -> 32, stays on sconv.hip: 383 vs 366 us here,
+  // profiles/r05w_nconv_micro.jsonl)
   if (!s2 && !k1) return DCVC_HIP_EUNSUPPORTED;
   if (a->shuffle && (!k1 || a->cout % 4 || a->res.ptr || a->res2.ptr)) return DCVC_HIP_EUNSUPPORTED;
   if (a->res2.ptr && !a->res.ptr) return DCVC_HIP_EUNSUPPORTED;

@@ -1,16 +1,11 @@
-// Thin convolutions in fp32 VALU arithmetic: the layers whose input or
-// output has only a few channels, where a 16 x 16 x 32 MFMA tile is mostly
-// padding (the split kernels' 16-row output block carries 2 or 3 channels, or
-// their 32-channel K step 2):
-//   * few input channels (tconv_ci_kernel, the default route): the motion
-//     encoder's first ResidualBlockWithStride on the 2-channel flow, 3x3 /
-//     1x1 stride 2, 2 -> 64 (video_model.py:121-140, layers.py
-//     ResidualBlockWithStride): 125 -> 58 us and 143 -> 29 us at 1080p
-//     (profiles/r05r_tconv_ci_micro.jsonl);
-//   * few output channels (tconv_co_kernel, only with dcvc_set_option("tconv",
-//     2)): SpyNet's last 7x7 of every basic module, 16 -> 2
-//     (DCVC-DC/src/models/video_net.py:79-100), and the reconstruction heads'
-//     48 -> 3 3x3 -- slower than sconv.hip there (see dcvc_internal_tconv).
+// Thin convolutions in fp32 VALU arithmetic: the layers with 2 input
+// channels, where a 32-deep MFMA K step would be 94 % padding: the motion
+// encoder's first ResidualBlockWithStride on the 2-channel flow, 3x3 / 1x1
+// stride 2, 2 -> 64 (DCVC-DC/src/models/video_model.py:121-140, layers.py
+// ResidualBlockWithStride): 125 -> 58 us and 143 -> 29 us at 1080p against
+// sconv.hip (profiles/r05r_tconv_ci_micro.jsonl).  (The few-output-channel
+// layers have an MFMA kernel of their own, nconv.hip; an fp32-VALU one lost
+// to sconv there)
 // The weights are read from the split-packed buffer the layer already has
 // (dcvc_conv_pack_weights' F16X3 layout) and rebuilt in LDS as hi + 2^-11 lo,
 // a 22-bit fp32 value (the split kernels' products drop the lo x lo term
@@ -38,7 +33,7 @@ struct TP {
   int act;
   float slope;
   int vec_out;
-  int nq;               // (co kernel) pixel quads per output row
+  int nq;               // pixel quads per output row
 };
 
 // w(n, tap, ci) of dcvc_conv_pack_weights' F16X3 layout: 32-channel chunks,
@@ -81,97 +76,6 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t xrsrc(const TP &p) {
                                            (int)((int64_t)p.H * p.W * p.xcs * 4), 0x00020000);
 }
 constexpr int kOob = 0x7ffffff0;
-
-// ---- few output channels (stride 1): thread = 4 consecutive output pixels
-// of a row, all COUT channels; per K step (tap row dy, 4-channel group c4)
-// the 4 + KS - 1 input columns are loaded once (16-byte buffer loads, zeros
-// outside the image) and used by the KS taps of all 4 pixels; the loads of
-// step s + 1 are in flight while step s computes.  LDS: the weights as
-// [dy][dx][c4][co] float4 (every lane reads the same address).
-template <int KS, int COUT, bool INL>
-__global__ void __launch_bounds__(256) tconv_co_kernel(TP p) {
-  extern __shared__ __align__(16) unsigned char smem[];
-  f32x4 *Lw = reinterpret_cast<f32x4 *>(smem);
-  const int C4 = p.cin >> 2;
-  // (no loop vectorization: packed-f32 instructions are kept out of the
-  // library, scripts/check_isa.sh)
-#pragma clang loop vectorize(disable) interleave(disable)
-  for (int i = threadIdx.x; i < KS * KS * C4 * COUT; i += 256) {
-    const int co = i % COUT, r = i / COUT, c4 = r % C4, tap = r / C4;
-    f32x4 v;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) v[e] = packed_w(p.w, co, tap, 4 * c4 + e, p.cin, p.cout, p.kt);
-    Lw[i] = v;
-  }
-  __syncthreads();
-  const int64_t gid = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (gid >= (int64_t)p.Ho * p.nq) return;
-  const int oy = (int)(gid / p.nq), ox0 = (int)(gid - (int64_t)oy * p.nq) * 4;
-  constexpr int NC = 4 + KS - 1;
-  const __amdgpu_buffer_rsrc_t xr = xrsrc(p);
-  int cof[NC];   // byte offsets of the window's columns (kOob outside the image)
-#pragma unroll
-  for (int j = 0; j < NC; ++j) {
-    const int ix = ox0 + j - p.pad;
-    cof[j] = (unsigned)ix < (unsigned)p.W ? (ix * p.xcs + p.xco) * 4 : -1;
-  }
-  const int NS = KS * C4;
-  auto load = [&](f32x4 (&xv)[NC], int s) __attribute__((always_inline)) {
-    const int dy = s / C4, c4 = s - dy * C4;
-    const int iy = oy + dy - p.pad;
-    const int ro = (unsigned)iy < (unsigned)p.H ? iy * p.W * p.xcs * 4 + c4 * 16 : -1;
-#pragma unroll
-    for (int j = 0; j < NC; ++j) {
-      const int o = (ro < 0 || cof[j] < 0) ? kOob : ro + cof[j];
-      xv[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, o, 0, 0));
-    }
-  };
-  float acc[4][COUT];
-#pragma unroll
-  for (int k = 0; k < 4; ++k)
-#pragma unroll
-    for (int co = 0; co < COUT; ++co) acc[k][co] = 0.f;
-  auto step = [&](f32x4 (&xv)[NC], int s) __attribute__((always_inline)) {
-    const int dy = s / C4, c4 = s - dy * C4;
-    if constexpr (INL) {
-#pragma unroll
-      for (int j = 0; j < NC; ++j)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) xv[j][e] = fmaxf(xv[j][e], xv[j][e] * p.in_slope);
-    }
-    const f32x4 *wr = Lw + ((dy * KS) * C4 + c4) * COUT;
-#pragma unroll
-    for (int dx = 0; dx < KS; ++dx)
-#pragma unroll
-      for (int co = 0; co < COUT; ++co) {
-        const f32x4 wv = wr[dx * C4 * COUT + co];
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-#pragma unroll
-          for (int e = 0; e < 4; ++e) acc[k][co] = __builtin_fmaf(wv[e], xv[k + dx][e], acc[k][co]);
-      }
-  };
-  f32x4 xa[NC], xb[NC];
-  load(xa, 0);
-  for (int s = 0; s < NS; s += 2) {
-    const bool two = s + 1 < NS;
-    if (two) load(xb, s + 1);
-    step(xa, s);
-    if (two) {
-      if (s + 2 < NS) load(xa, s + 2);
-      step(xb, s + 1);
-    }
-  }
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const int ox = ox0 + k;
-    if (ox >= p.Wo) break;
-    const int64_t pix = (int64_t)oy * p.Wo + ox;
-    float *yp = p.y + pix * p.ycs + p.yco;
-#pragma unroll
-    for (int co = 0; co < COUT; ++co) yp[co] = epi(p, acc[k][co], co, pix);
-  }
-}
 
 // ---- few input channels: thread = (16 output channels, 4 consecutive output
 // pixels of a row); lane g of a pixel quad's 4 lanes owns the channels
@@ -260,7 +164,7 @@ __global__ void __launch_bounds__(256) tconv_ci_kernel(TP p) {
   }
 }
 
-int g_enable = 1;   // dcvc_set_option("tconv", v): 0 = off (split kernels), 1 = 2-channel inputs, 2 = also <= 4-channel outputs
+int g_enable = 1;   // dcvc_set_option("tconv", 0): these layers to the split kernels
 
 template <typename K>
 int launch(K kern, const char *name, int64_t threads, size_t lds, const TP &p, hipStream_t st) {
@@ -279,9 +183,8 @@ int launch(K kern, const char *name, int64_t threads, size_t lds, const TP &p, h
 extern "C" void dcvc_internal_tconv_enable(int v) { g_enable = v; }
 
 // Thin split-precision convolutions (dcvc_conv2d tries it first for
-// DCVC_F16X3 weights): stride-1 3x3 / 7x7 layers with <= 4 output channels
-// and a 4-aligned input view, and 2-channel-input 3x3 / 1x1 layers of a
-// multiple of 64 output channels.  DCVC_HIP_EUNSUPPORTED otherwise.
+// DCVC_F16X3 weights): 2-channel-input 3x3 / 1x1 layers of a multiple of 64
+// output channels.  DCVC_HIP_EUNSUPPORTED otherwise.
 extern "C" int dcvc_internal_tconv(const dcvc_conv_args *a, void *stream) {
   if (!g_enable) return DCVC_HIP_EUNSUPPORTED;
   if (a->kh != a->kw || a->pad != a->kh / 2 || a->shuffle) return DCVC_HIP_EUNSUPPORTED;
@@ -289,15 +192,9 @@ extern "C" int dcvc_internal_tconv(const dcvc_conv_args *a, void *stream) {
   if (a->in_op != DCVC_IN_NONE && !(a->in_op == DCVC_IN_LRELU)) return DCVC_HIP_EUNSUPPORTED;
   if (a->res2.ptr && !a->res.ptr) return DCVC_HIP_EUNSUPPORTED;
   if ((a->res.ptr && a->res.dtype != DCVC_F32) || (a->res2.ptr && a->res2.dtype != DCVC_F32)) return DCVC_HIP_EUNSUPPORTED;
-  const bool co = a->stride == 1 && (a->kh == 3 || a->kh == 7) && a->cout <= 4 && a->cin % 4 == 0 && a->cin <= 64 &&
-                  (uintptr_t)a->x.ptr % 16 == 0 && a->x.cstride % 4 == 0 && a->x.coff % 4 == 0;
   const bool ci = a->cin == 2 && (a->kh == 3 || a->kh == 1) && a->cout % 64 == 0 && a->cout <= 256 &&
                   (a->stride == 1 || a->stride == 2);
-  // the few-output-channel kernel loses to sconv.hip at the codec's shapes
-  // (16 -> 2 7x7 at 1080p 652 vs 380 us, 48 -> 3 3x3 1238 vs 206 us,
-  // profiles/r05q_tconv_micro.jsonl: its 16-byte column loads thrash L1):
-  // only on request (dcvc_set_option("tconv", 2))
-  if (!ci && !(co && g_enable == 2)) return DCVC_HIP_EUNSUPPORTED;
+  if (!ci) return DCVC_HIP_EUNSUPPORTED;
   TP p{};
   p.x = reinterpret_cast<const float *>(a->x.ptr);
   p.H = a->x.H;
@@ -339,18 +236,6 @@ extern "C" int dcvc_internal_tconv(const dcvc_conv_args *a, void *stream) {
   if ((int64_t)p.H * p.W * p.xcs * 4 >= ((int64_t)1 << 31) - 64) return DCVC_HIP_EUNSUPPORTED;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const int64_t quads = (int64_t)p.Ho * p.nq;
-  if (co) {
-    const size_t lds = (size_t)a->kh * a->kw * (a->cin / 4) * a->cout * 16;
-#define TCO(KS, CO)                                                                                    \
-  if (a->kh == KS && a->cout == CO)                                                                    \
-    return p.in_lrelu ? launch(tconv_co_kernel<KS, CO, true>, "tconv_co_kernel<" #KS ", " #CO ", true>", \
-                               quads, lds, p, st)                                                      \
-                      : launch(tconv_co_kernel<KS, CO, false>, "tconv_co_kernel<" #KS ", " #CO ", false>", \
-                               quads, lds, p, st);
-    TCO(3, 1) TCO(3, 2) TCO(3, 3) TCO(3, 4) TCO(7, 1) TCO(7, 2) TCO(7, 3) TCO(7, 4)
-#undef TCO
-    return DCVC_HIP_EUNSUPPORTED;
-  }
   const size_t lds = (size_t)a->kh * a->kw * 2 * a->cout * 4;
   const int64_t threads = quads * (a->cout / 64) * 4;
 #define TCI(KS, S)                                                                                     \

@@ -31,10 +31,12 @@ def _gpu():
     hip.set_option("xconv", 0)
     hip.set_option("dconv", 0)
     hip.set_option("tconv", 0)
+    hip.set_option("nconv", 0)
     yield
     hip.set_option("xconv", 1)
     hip.set_option("dconv", 1)
     hip.set_option("tconv", 1)
+    hip.set_option("nconv", 1)
 
 
 def K():
