@@ -422,10 +422,17 @@ xconv3_kernel(XP p) {
       // zero weights: any finite data, tap 0)
       constexpr int ta = tpk * rr, tb = tpk * rr + 1;
       constexpr int ta_ = ta < KT ? ta : 0, tb_ = tb < KT ? tb : 0;
-      static_assert(tpk == 2, "4-tap packing (<= 8-channel chunks) is not instantiated");
       const int oA = bo2[ta_ % KS] + (ta_ / KS) * IWP * 32;
       const int oB = bo2[tb_ % KS] + (tb_ / KS) * IWP * 32;
-      const int o0 = sub ? oB : oA;
+      int o0 = sub ? oB : oA;
+      if constexpr (tpk == 4) {
+        // (8-channel last chunk: four taps per K step, one per lane group)
+        constexpr int tc = tpk * rr + 2, td = tpk * rr + 3;
+        constexpr int tc_ = tc < KT ? tc : 0, td_ = td < KT ? td : 0;
+        const int oC = bo2[tc_ % KS] + (tc_ / KS) * IWP * 32;
+        const int oD = bo2[td_ % KS] + (td_ / KS) * IWP * 32;
+        o0 = sub == 0 ? oA : sub == 1 ? oB : sub == 2 ? oC : oD;
+      }
 #pragma unroll
       for (int r = 0; r < RW; ++r) {
         const int o = o0 + r * IWP * 32;
@@ -851,7 +858,7 @@ int g_enable = 1;   // dcvc_set_option("xconv", 0): route every split conv to sc
 // publish, 32 no image-operand reads, 64 no image loads, 128 no residual loads
 // and output stores
 int g_dbg = 0;
-int g_rw1 = 0;
+int g_rw1 = 1;
 
 template <int CIN, int BN, int RW, int NW, int NRES, bool SHUF = false, int KS = 3>
 int launch(XP p, hipStream_t st) {
@@ -911,10 +918,12 @@ int pick_bn(XP p, hipStream_t st) {
     if (p.cout % 48 == 0) return launch<CIN, 48, 2, 8, 0, true>(p, st);
     return launch<CIN, 32, 2, 8, 0, true>(p, st);
   }
-  if constexpr (CIN == 64 || CIN == 128) {
+  if constexpr (CIN == 64) {
     // residual layers of 64-channel multiples: 8-row tiles (one row per wave)
     // of 64-channel blocks instead of 16-row tiles of 32-channel blocks, which
-    // load and split the input once per block (A/B: "xconv_rw1")
+    // load and split the input once per block: 64 -> 64 + residual at 544 x
+    // 960 4-6 %, 64 -> 128 3 % faster; 128 -> 128 at 272 x 480 1 % slower, so
+    // 64 input channels only (profiles/r05u_xconv_rw1_ab.jsonl; "xconv_rw1" 0: off)
     if (g_rw1 && p.has_res && p.cout % 64 == 0) return pick_res<CIN, 64, 1, 8, RES_OK>(p, st);
   }
   if (p.cout == 32 || p.cout == 48) return p.cout == 32 ? pick_res<CIN, 32, 2, 8, RES_OK>(p, st) : pick_res<CIN, 48, 2, 8, RES_OK>(p, st);
@@ -1039,6 +1048,7 @@ extern "C" int dcvc_internal_xconv(const dcvc_conv_args *a, void *stream) {
     // SpyNet's 7x7 layers (video_net.py:79-100): the halo image of a 22 x 22
     // pixel tile leaves LDS for a weight ring of 16- or 32-channel blocks
     switch (a->cin) {
+      case 8: return a->cout % 32 == 0 ? launch<8, 32, 2, 8, 0, false, 7>(p, st) : DCVC_HIP_EUNSUPPORTED;
       case 16: return a->cout == 16 ? launch<16, 16, 2, 8, 0, false, 7>(p, st)
                                     : a->cout % 32 == 0 ? launch<16, 32, 2, 8, 0, false, 7>(p, st) : DCVC_HIP_EUNSUPPORTED;
       case 32: return a->cout == 16 ? launch<32, 16, 2, 8, 0, false, 7>(p, st)

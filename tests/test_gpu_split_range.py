@@ -36,8 +36,8 @@ def rel_err(got, ref):
 
 # (cin, cout, k, stride, kernel family expected)
 CONVS = [(48, 48, 3, 1, "xconv3_kernel"), (6, 64, 3, 1, "sconv_kernel"), (56, 64, 3, 2, "dconv_kernel"),
-         (32, 64, 7, 1, "xconv3_kernel"), (8, 32, 7, 1, "sconv_kernel"), (96, 48, 1, 1, "sgemm_kernel"),
-         (64, 48, 3, 2, "dconv_kernel")]
+         (32, 64, 7, 1, "xconv3_kernel"), (8, 32, 7, 1, "xconv3_kernel"), (96, 48, 1, 1, "sgemm_kernel"),
+         (64, 48, 3, 2, "dconv_kernel"), (8, 48, 7, 1, "sconv_kernel")]
 
 
 @pytest.mark.parametrize("case", CONVS)

@@ -183,6 +183,8 @@ K7_CASES = [
     (32, 16, 21, 35, 0.0),
     (16, 32, 18, 40, 0.1),
     (64, 32, 136, 240, None),   # many tiles per workgroup
+    (8, 32, 36, 70, 0.0),       # SpyNet's first layer (2 frames + flow): 4 taps per K step
+    (8, 32, 136, 240, 0.0),
 ]
 
 
