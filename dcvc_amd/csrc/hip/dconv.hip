@@ -373,6 +373,7 @@ int g_cus = 0;
 int g_enable = 1;   // dcvc_set_option("dconv", 0): route these layers to sconv.hip
 int g_k1 = 1;       // dcvc_set_option("dconv_1x1", 0): stride-1 1x1 layers to sgemm.hip
 int g_bn128 = 1;   // dcvc_set_option("dconv_bn128", 0): 64-channel n-blocks for 1x1 layers (A/B)
+int g_s2blk = 2;   // dcvc_set_option("dconv_s2blocks", n): most n-blocks of a 3x3 layer (A/B)
 int g_xcd = 1;      // dcvc_set_option("dconv_xcd", 0): n-blocks of a tile on different XCDs (A/B)
 
 template <int KS, int BN, int NP>
@@ -414,7 +415,7 @@ int launch(DP p, hipStream_t st) {
 template <int KS, int NP>
 int pick(DP p, hipStream_t st) {
   auto fits = [&](int bn) {
-    return (size_t)p.nst * 2 * bn * 32 * 2 + (size_t)2 * bn * 4 <= 160 * 1024 && (KS == 1 || 2 * bn >= p.cout);
+    return (size_t)p.nst * 2 * bn * 32 * 2 + (size_t)2 * bn * 4 <= 160 * 1024 && (KS == 1 || g_s2blk * bn >= p.cout);
   };
   if (p.cout % 16) return fits(16) ? launch<KS, 16, NP>(p, st) : DCVC_HIP_EUNSUPPORTED;
   // (1x1 with 128-channel multiples: one 128-row block of one 16-pixel group
@@ -434,6 +435,7 @@ int pick(DP p, hipStream_t st) {
 extern "C" void dcvc_internal_dconv_enable(int v) { g_enable = v; }
 extern "C" void dcvc_internal_dconv_1x1(int v) { g_k1 = v; }
 extern "C" void dcvc_internal_dconv_xcd(int v) { g_xcd = v; }
+extern "C" void dcvc_internal_dconv_s2blocks(int v) { g_s2blk = v; }
 extern "C" void dcvc_internal_dconv_bn128(int v) { g_bn128 = v; }
 
 // Stride-2 3x3 / 1x1 and feature-rate 1x1 f16x3 convolutions with fp32
