@@ -597,6 +597,7 @@ extern "C" void dcvc_internal_sffn128(int v);
 extern "C" void dcvc_internal_dconv_enable(int v);
 extern "C" void dcvc_internal_dconv_1x1(int v);
 extern "C" void dcvc_internal_dconv_xcd(int v);
+extern "C" void dcvc_internal_dconv_gate(int v);
 extern "C" void dcvc_internal_dconv_s2blocks(int v);
 extern "C" void dcvc_internal_dconv_bn128(int v);
 
@@ -847,6 +848,10 @@ extern "C" int dcvc_set_option(const char *name, int value) {
   }
   if (std::strcmp(name, "dconv_xcd") == 0) {
     dcvc_internal_dconv_xcd(value);
+    return DCVC_HIP_OK;
+  }
+  if (std::strcmp(name, "dconv_gate") == 0) {
+    dcvc_internal_dconv_gate(value);
     return DCVC_HIP_OK;
   }
   if (std::strcmp(name, "dconv_s2blocks") == 0) {

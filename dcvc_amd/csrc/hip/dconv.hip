@@ -68,7 +68,7 @@ __device__ __forceinline__ void sfor(F &&f) {
   sfor_(f, std::make_integer_sequence<int, N>{});
 }
 
-template <int KS, int BN, int NP>
+template <int KS, int BN, int NP, bool GATE>
 __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) dconv_kernel(DP p) {
   typedef DG<KS, BN, NP> G;
   constexpr int NT = G::NT, NW = G::NW;
@@ -155,8 +155,10 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
       lx = (ta - ly * p.nseg) * (16 * NP);
     }
   };
-  // B-operand raw loads of the next (tile, step) into pr
-  auto load = [&](float (&pr)[NP][8]) __attribute__((always_inline)) {
+  // B-operand raw loads of the next (tile, step) into pr (GATE: the gate
+  // half of the input, channels cin + ch .., in pr[j][8 ..])
+  constexpr int PW = GATE ? 16 : 8;
+  auto load = [&](float (&pr)[NP][PW]) __attribute__((always_inline)) {
     int tap, ch;
     if (lc < p.nch - 1) {
       tap = lr;
@@ -181,11 +183,21 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
         pr[j][e] = a[e];
         pr[j][4 + e] = b[e];
       }
+      if constexpr (GATE) {
+        const int og = ok ? o + p.cin * 4 : 0x7fffffe0;
+        const f32x4 ga = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, og, 0, 0));
+        const f32x4 gb = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, og + 16, 0, 0));
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          pr[j][8 + e] = ga[e];
+          pr[j][12 + e] = gb[e];
+        }
+      }
     }
   };
   // DEPTH steps of operand loads in flight (the L2 / HBM latency of a
   // step's loads is covered by the MFMAs of the DEPTH - 1 steps before it)
-  float pr[DEPTH][NP][8];
+  float pr[DEPTH][NP][PW];
 #pragma unroll
   for (int d = 0; d < DEPTH; ++d) {
     load(pr[d]);
@@ -203,11 +215,18 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
   };
   zero();
   // one K step from the raw operands pr (then refilled with the step two ahead)
-  auto step = [&](int st, float (&pr)[NP][8]) __attribute__((always_inline)) {
+  auto step = [&](int st, float (&pr)[NP][PW]) __attribute__((always_inline)) {
     f16x8 bh[NP], bl[NP];
 #pragma unroll
     for (int j = 0; j < NP; ++j) {
-      if (p.in_lrelu) {
+      if constexpr (GATE) {
+        // ConvFFN2's gate (sconv.hip's order): x1 * lrelu(x2)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float gv = pr[j][8 + e];
+          pr[j][e] = pr[j][e] * (gv >= 0.f ? gv : gv * p.in_slope);
+        }
+      } else if (p.in_lrelu) {
 #pragma unroll
         for (int e = 0; e < 8; ++e) pr[j][e] = lrelu_in(pr[j][e], p.in_slope);
       }
@@ -374,9 +393,10 @@ int g_enable = 1;   // dcvc_set_option("dconv", 0): route these layers to sconv.
 int g_k1 = 1;       // dcvc_set_option("dconv_1x1", 0): stride-1 1x1 layers to sgemm.hip
 int g_bn128 = 1;   // dcvc_set_option("dconv_bn128", 0): 64-channel n-blocks for 1x1 layers (A/B)
 int g_s2blk = 2;   // dcvc_set_option("dconv_s2blocks", n): most n-blocks of a 3x3 layer (A/B)
+int g_gate = 1;     // dcvc_set_option("dconv_gate", 0): ConvFFN2's gated 1x1 to sconv.hip
 int g_xcd = 1;      // dcvc_set_option("dconv_xcd", 0): n-blocks of a tile on different XCDs (A/B)
 
-template <int KS, int BN, int NP>
+template <int KS, int BN, int NP, bool GATE = false>
 int launch(DP p, hipStream_t st) {
   const size_t lds = (size_t)p.nst * 2 * BN * 32 * 2 + (size_t)2 * BN * 4;
   if (lds > 160 * 1024) return DCVC_HIP_EUNSUPPORTED;
@@ -401,8 +421,8 @@ int launch(DP p, hipStream_t st) {
   if (per < 1) per = 1;
   const int64_t grid = per * p.nblk;
   p.xcd = p.nblk > 1 && g_xcd && grid % (8 * p.nblk) == 0;
-  auto kern = dconv_kernel<KS, BN, NP>;
-  dcvc_note_kernel("dconv_kernel<%d, %d, %d>@%lld", KS, BN, NP, (long long)grid * 512);
+  auto kern = dconv_kernel<KS, BN, NP, GATE>;
+  dcvc_note_kernel("dconv_kernel<%d, %d, %d, %s>@%lld", KS, BN, NP, GATE ? "true" : "false", (long long)grid * 512);
   dcvc_ensure_lds(reinterpret_cast<const void *>(kern), 160 * 1024);
   hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(512), lds, st, p);
   DCVC_LAUNCH_CHECK();
@@ -412,6 +432,18 @@ int launch(DP p, hipStream_t st) {
 // n-block: all of cout when its weights fit LDS, else the widest of 64 / 48 /
 // 32 / 16 that does (each block then re-reads the input: more than two
 // blocks of a 3x3 layer lose to sconv.hip's halo image)
+// ConvFFN2's gated second 1x1 (in_op DCVC_IN_GATE: x1 * lrelu(x2) of the
+// two halves of a 2 cin-channel input): one 16-pixel group per wave, the
+// gate half's loads beside the value half's
+int pick_gate(DP p, hipStream_t st) {
+  auto fits = [&](int bn) { return (size_t)p.nst * 2 * bn * 32 * 2 + (size_t)2 * bn * 4 <= 160 * 1024; };
+  if (p.cout % 64 == 0 && fits(64)) return launch<1, 64, 1, true>(p, st);
+  if (p.cout % 48 == 0 && fits(48)) return launch<1, 48, 1, true>(p, st);
+  if (p.cout % 32 == 0 && fits(32)) return launch<1, 32, 1, true>(p, st);
+  if (fits(16)) return launch<1, 16, 1, true>(p, st);
+  return DCVC_HIP_EUNSUPPORTED;
+}
+
 template <int KS, int NP>
 int pick(DP p, hipStream_t st) {
   auto fits = [&](int bn) {
@@ -435,6 +467,7 @@ int pick(DP p, hipStream_t st) {
 extern "C" void dcvc_internal_dconv_enable(int v) { g_enable = v; }
 extern "C" void dcvc_internal_dconv_1x1(int v) { g_k1 = v; }
 extern "C" void dcvc_internal_dconv_xcd(int v) { g_xcd = v; }
+extern "C" void dcvc_internal_dconv_gate(int v) { g_gate = v; }
 extern "C" void dcvc_internal_dconv_s2blocks(int v) { g_s2blk = v; }
 extern "C" void dcvc_internal_dconv_bn128(int v) { g_bn128 = v; }
 
@@ -458,7 +491,9 @@ extern "C" int dcvc_internal_dconv(const dcvc_conv_args *a, void *stream) {
   if (!s2 && !k1) return DCVC_HIP_EUNSUPPORTED;
   if (a->shuffle && (!k1 || a->cout % 4 || a->res.ptr || a->res2.ptr)) return DCVC_HIP_EUNSUPPORTED;
   if (a->res2.ptr && !a->res.ptr) return DCVC_HIP_EUNSUPPORTED;
-  if (a->in_op != DCVC_IN_NONE && !(a->in_op == DCVC_IN_LRELU && a->in_slope >= 0.f && a->in_slope <= 1.f))
+  const bool gate = a->in_op == DCVC_IN_GATE;
+  if (gate && (!k1 || !g_gate || a->shuffle)) return DCVC_HIP_EUNSUPPORTED;
+  if (a->in_op != DCVC_IN_NONE && !gate && !(a->in_op == DCVC_IN_LRELU && a->in_slope >= 0.f && a->in_slope <= 1.f))
     return DCVC_HIP_EUNSUPPORTED;
   if (a->act != DCVC_ACT_NONE && !(a->act == DCVC_ACT_LRELU && a->slope >= 0.f && a->slope <= 1.f))
     return DCVC_HIP_EUNSUPPORTED;
@@ -524,6 +559,7 @@ extern "C" int dcvc_internal_dconv(const dcvc_conv_args *a, void *stream) {
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   // cout < 16: one 16-row block, rows past cout are zero weights, their
   // outputs not stored
+  if (gate) return pick_gate(p, st);
   switch (a->kh) {
     case 1: return pick<1, 2>(p, st);
     case 3: return pick<3, 2>(p, st);

@@ -59,8 +59,8 @@ CASES = [
     (64, 8, 1, 1, 256, 260, False, False, 0, True),
     (64, 8, 1, 1, 256, 263, True, True, 0, True),
 ]
-# shapes dconv leaves to sconv / sgemm (more than two output-channel blocks of
-# a 3x3 stride-2 layer; latent-rate 1x1)
+# shapes dconv leaves to sconv / sgemm / xconv (more than two output-channel
+# blocks of a 3x3 stride-2 layer; latent-rate 1x1; SpyNet's 8 -> 32 7x7)
 FALLBACK = [(128, 96, 3, 2, 34, 60), (8, 32, 7, 1, 40, 50), (192, 96, 3, 2, 17, 31), (384, 384, 1, 1, 68, 120), (1024, 256, 1, 1, 17, 30)]
 
 
@@ -72,7 +72,7 @@ def test_dconv_leaves_shapes_it_loses_on(case):
     h.conv(cw, h.from_nchw(torch.randn(1, cin, H, W), h.F32), out_dtype=h.F32)
     torch.cuda.synchronize()
     kern = h.lib().dcvc_last_kernel().decode()
-    assert kern.startswith(("sconv_kernel", "sgemm_kernel")), kern
+    assert kern.startswith(("sconv_kernel", "sgemm_kernel", "xconv3_kernel")), kern
 
 
 @pytest.mark.parametrize("case", CASES)
@@ -173,7 +173,38 @@ def test_dconv_bn128_matches_sgemm(case):
             h.set_option("dconv", 1)
         outs.append((kern, y.buf.cpu()))
     big = H * W >= 65536
-    assert outs[0][0].startswith("dconv_kernel<1, 128, 1>" if big else ("sgemm_kernel", "sconv_kernel")), outs[0][0]
-    assert outs[1][0].startswith("dconv_kernel<1, 64, 2>" if big else ("sgemm_kernel", "sconv_kernel")), outs[1][0]
+    assert outs[0][0].startswith("dconv_kernel<1, 128, 1," if big else ("sgemm_kernel", "sconv_kernel")), outs[0][0]
+    assert outs[1][0].startswith("dconv_kernel<1, 64, 2," if big else ("sgemm_kernel", "sconv_kernel")), outs[1][0]
     assert outs[2][0].startswith(("sgemm_kernel", "sconv_kernel")), outs[2][0]
     assert torch.equal(outs[0][1], outs[2][1]) and torch.equal(outs[1][1], outs[2][1])
+
+
+@pytest.mark.parametrize("cin,cout,H,W", [(64, 64, 256, 260), (96, 48, 272, 250), (128, 32, 256, 257), (64, 16, 260, 256)])
+def test_dconv_gated_1x1_matches_sconv(cin, cout, H, W):
+    """ConvFFN2's gated second 1x1 (DCVC-DC/src/models/layers.py:182-197:
+    conv_out(x1 * lrelu(x2)) + x, in_op DCVC_IN_GATE on a 2 cin-channel
+    input): dconv against sconv.hip's gated path, bit for bit, and fp64."""
+    h = K()
+    g = torch.Generator().manual_seed(cin + cout + H)
+    x = torch.randn(1, 2 * cin, H, W, generator=g)
+    w = torch.randn(cout, cin, 1, 1, generator=g) / cin ** 0.5
+    b = torch.randn(cout, generator=g) * 0.1
+    r = torch.randn(1, cout, H, W, generator=g)
+    xd = x.double()
+    gated = xd[:, :cin] * F.leaky_relu(xd[:, cin:], 0.1)
+    ref = r.double() + F.conv2d(gated, w.double(), b.double())
+    cw = h.ConvW(w, b, 1, h.F16X3)
+    xa, ra = h.from_nchw(x, h.F32), h.from_nchw(r, h.F32)
+    outs = []
+    for on in (1, 0):
+        h.set_option("dconv", on)
+        try:
+            y = h.conv(cw, xa, out_dtype=h.F32, in_op=h.IN_GATE, in_slope=0.1, res=ra)
+            torch.cuda.synchronize()
+            kern = h.lib().dcvc_last_kernel().decode()
+        finally:
+            h.set_option("dconv", 1)
+        assert (kern.startswith("dconv_kernel<1") and ", true>" in kern) if on else kern.startswith("sconv_kernel"), kern
+        outs.append(y.nchw().cpu())
+    assert rel_err(outs[0], ref) < TOL
+    assert torch.equal(outs[0], outs[1])
