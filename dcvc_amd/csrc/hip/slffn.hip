@@ -508,7 +508,8 @@ extern "C" int dcvc_dw_conv2_split(const dcvc_dwc_args *a, void *stream) {
   if (a->t.dtype != DCVC_F32 || a->r.dtype != DCVC_F32 || a->y.dtype != DCVC_F32 || a->t.C != c || a->r.C != c ||
       a->y.C != c || a->t.H != a->y.H || a->t.W != a->y.W || a->r.H != a->y.H || a->r.W != a->y.W)
     return DCVC_HIP_EINVAL;
-  if (c != 192 && c != 384) return DCVC_HIP_EUNSUPPORTED;
+  // (128: the feature-rate blocks at 1/4 resolution, dcvc_amd/layers.py DW128)
+  if (c != 192 && c != 384 && c != 128) return DCVC_HIP_EUNSUPPORTED;
   auto al = [](const dcvc_tensor &v) { return (uintptr_t)v.ptr % 16 == 0 && v.cstride % 4 == 0 && v.coff % 4 == 0; };
   if (!al(a->t) || !al(a->r) || !al(a->y) || a->t.cstride % 8 || a->t.coff % 8) return DCVC_HIP_EUNSUPPORTED;
   const int64_t npix = (int64_t)a->t.H * a->t.W;
@@ -538,5 +539,5 @@ extern "C" int dcvc_dw_conv2_split(const dcvc_dwc_args *a, void *stream) {
   p.w2bytes = (int)((int64_t)c * c * 2 * 2);
   p.b2 = a->b2;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  return c == 384 ? run_dc<384>(p, st) : run_dc<192>(p, st);
+  return c == 384 ? run_dc<384>(p, st) : c == 192 ? run_dc<192>(p, st) : run_dc<128>(p, st);
 }

@@ -26,6 +26,7 @@ from .hip import Act, F32, BF16, F16X3, ACT_LRELU, ACT_NONE, IN_LRELU, IN_GATE
 FUSE_DCB = True   # fused DepthConvBlock kernel where instantiated (A/B switch)
 FUSE_FFN = True   # split precision: fused ConvFFN kernel (sffn.hip) where instantiated (A/B switch)
 FUSE_DC = True    # split precision: fused DepthConv kernel (sdc.hip) where instantiated (A/B switch)
+DW128 = True      # split precision: the 128-channel feature-rate DepthConv tail (depthwise + conv2 + identity) in one kernel (A/B)
 # (cin, cout, adaptor) of the fused DepthConv instantiations (sdc.hip supported())
 SDC_SHAPES = {(64, 48, True), (48, 32, True), (32, 64, True), (64, 64, False), (48, 48, False), (32, 32, False)}
 
@@ -237,8 +238,8 @@ class DepthConvBlock:
         # split precision, the entropy model's adaptor-free 192 / 384-channel
         # latent blocks: depthwise + conv2 + identity in one kernel (slffn.hip)
         self.dwc = None
-        if (FUSE_DC and latent and self.conv1.compute == F16X3 and self.adaptor is None
-                and self.conv1.cin == self.conv2.cout and self.conv2.cin in (192, 384)):
+        if (FUSE_DC and self.conv1.compute == F16X3 and self.adaptor is None and self.conv1.cin == self.conv2.cout
+                and ((latent and self.conv2.cin in (192, 384)) or (DW128 and not latent and self.conv2.cin == 128))):
             self.dwc = K.DwcW(self.dw[0], self.dw[1], sd[d + ".conv2.weight"], sd[d + ".conv2.bias"], ctx.dev)
         self.ffn = None
         # (sffn.hip for the feature-rate widths; slffn.hip for the latent

@@ -61,6 +61,23 @@ def main():
             run = lambda: K.depth_conv_split(dw, x, y)  # noqa: E731
             fl = 2.0 * H * W * (cin * cin + 9 * cin + cin * cout * (2 if ad else 1))
             nb = 4 * H * W * (cin + cout) + dw.w.numel() * 2
+        elif kind in ("dwc", "dwu"):
+            # the DepthConv tail (depthwise + conv2 + identity): fused (sldc.hip,
+            # dcvc_dw_conv2_split) or unfused (dwconv3x3, then the 1x1 with the residual)
+            c = int(m.group(2))
+            r = lambda *s: torch.randn(*s) * 0.2  # noqa: E731
+            w9, bd, w2, b2 = r(9, c).contiguous().to(dev), r(c).to(dev), r(c, c, 1, 1), r(c)
+            dwc = K.DwcW(w9, bd, w2, b2, dev)
+            cw2 = K.ConvW(w2, b2, 1, K.F16X3, dev)
+            t = K.from_nchw(torch.randn(1, c, H, W, device=dev), K.F32)
+            x = K.from_nchw(torch.randn(1, c, H, W, device=dev), K.F32)
+            y = K.empty(H, W, c, K.F32, dev)
+            if kind == "dwc":
+                run = lambda: K.dw_conv2_split(dwc, t, x, y)  # noqa: E731
+            else:
+                run = lambda: K.conv(cw2, K.dwconv3x3(t, w9, bd), y, res=x)  # noqa: E731
+            fl = 2.0 * H * W * c * (9 + c)
+            nb = 4 * H * W * 3 * c
         elif kind in ("od", "odr"):
             # odr: offsets spread like the bench codec's random-weight ones
             # (40 tanh(o) scattered over tens of pixels); od: small, smooth

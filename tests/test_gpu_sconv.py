@@ -367,7 +367,8 @@ def test_latent_ffn_matches_fp64_and_unfused(c, H, W):
     assert torch.equal(y2.nchw().cpu(), got)
 
 
-@pytest.mark.parametrize("c,H,W", [(384, 68, 120), (192, 68, 120), (384, 17, 30), (192, 5, 7), (384, 1, 40)])
+@pytest.mark.parametrize("c,H,W", [(384, 68, 120), (192, 68, 120), (384, 17, 30), (192, 5, 7), (384, 1, 40),
+                                   (128, 272, 480), (128, 37, 53)])
 def test_latent_dw_conv2_matches_fp64_and_unfused(c, H, W):
     """sldc_kernel (slffn.hip): the tail of a latent DepthConv, conv2(dw3x3(t)
     + bdw) + b2 + x (DCVC-DC/src/models/layers.py:135-163), against fp64 and
