@@ -31,7 +31,10 @@
 // loads / stores with out-of-range offsets where there is nothing to move), so
 // the count of vector-memory operations younger than a stage's weight DMA is a
 // compile-time constant and the DMA is waited for with an exact vmcnt(N) that
-// never drains the younger image / residual loads.
+// never drains the younger image / residual loads.  Exact means issued AND
+// used: hipcc deletes a load whose value is dead, so a padding load counted
+// but never read (round 5 loaded a 16-channel chunk's image with the 32-channel
+// chunk's piece count) makes N too large and the wait pass early.
 #include "common.h"
 #include "split.h"
 
@@ -101,14 +104,25 @@ struct XG {
   static constexpr int WST = BN * 32;                       // halves per weight stage (hi or lo)
   static constexpr int NDMA = 2 * BN / 16;                  // 1-KiB LDS-DMA pieces per stage
   static constexpr int DPW = (NDMA + NW - 1) / NW;          // ... per wave (every wave issues DPW)
-  // vector-memory instructions per thread: image chunk loads, tile loads (res, res2), epilogue stores
-  static constexpr int NIMG = 2 * PPM;
+  // vector-memory instructions per thread: image chunk loads (two per piece of
+  // the chunk loaded: a last chunk of 8 or 16 channels has fewer pieces), tile
+  // loads (res, res2), epilogue stores
   static constexpr int NTILE = NRES * RW * NT;
   static constexpr int NSTORE = RW * NT;
+  // image loads of stage x: a chunk's first stage loads the next chunk (of
+  // this tile, or the next tile's first).  Exact, not an upper bound: a count
+  // above the loads really issued lets a vmcnt wait pass with the DMA it
+  // waits for still in flight (the round-5 ring race)
+  static constexpr int img_ops(int x) {
+    if (st_row_(x) != 0) return 0;
+    const int c = x < (CH - 1) * KT ? x / KT : CH - 1;
+    const int cl = c + 1 < CH ? c + 1 : 0;
+    return 2 * (cl == CH - 1 ? PPL : PPF);
+  }
   // vector-memory instructions per thread issued by stage x of a tile after
   // its weight DMA, and in all
   static constexpr int after_dma(int x) {
-    return (st_row_(x) == 0 ? NIMG : 0) + (x == 0 ? NTILE : 0) + (x == NST - 1 ? NSTORE : 0);
+    return img_ops(x) + (x == 0 ? NTILE : 0) + (x == NST - 1 ? NSTORE : 0);
   }
   static constexpr int all_ops(int x) { return DPW + after_dma(x); }
   static constexpr int st_row_(int x) { return x < (CH - 1) * KT ? x % KT : x - (CH - 1) * KT; }
@@ -155,19 +169,28 @@ struct XG {
   static constexpr int NSW_FIT = (LDS_WG - 2048 - 4 * IMG * 2 - 1024) / (2 * WST * 2);
   // the deepest ring that fits, has at most a tile's stages + 1 slots and
   // keeps every stage's count of younger vector-memory operations below 64
-  // (vmcnt is 6 bits)
+  // (vmcnt is 6 bits); preferably (6 slots or more) one whose depth divides
+  // the tile's stage count: every stage of every tile then uses the same slot,
+  // so the slot arithmetic and the LDS / DMA addresses built from it are
+  // compile-time (2-3 % faster on 48 -> 48)
+  static constexpr bool vm_ok(int n) {
+    for (int x = 0; x < NST; ++x)
+      if (bar(x) && wait_for(x, n - 1) >= 64) return false;
+    return true;
+  }
   static constexpr int pick_nsw() {
     int n = NSW_FIT < 12 ? NSW_FIT : 12;
     if (n > NST + 1) n = NST + 1;
-    for (; n > 4; --n) {
-      int worst = 0;
-      for (int x = 0; x < NST; ++x)
-        if (bar(x)) worst = wait_for(x, n - 1) > worst ? wait_for(x, n - 1) : worst;
-      if (worst < 64) break;
-    }
+#ifndef XCONV_RING_DYN
+    for (int d = n; d >= 6; --d)
+      if (NST % d == 0 && vm_ok(d)) return d;
+#endif
+    for (; n > 4; --n)
+      if (vm_ok(n)) break;
     return n;
   }
   static constexpr int NSW = pick_nsw(), AH = NSW - 1;
+  static constexpr bool RING_STATIC = NST % NSW == 0;
   static_assert(NSW >= 4, "weight ring too shallow");
   // LDS (halves): [2 image buffers][hi, lo][IMG] | [NSW weight slots][hi, lo][WST] | DMA sink 512 | consts
   static constexpr int L_W = 4 * IMG;
@@ -269,18 +292,16 @@ xconv3_kernel(XP p) {
         __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(p.x + eb), (short)0, (int)nrec, 0x00020000);
     const int toff = ((iy0 - rb) * p.W + ix0) * p.xcs;
     const bool inner = iy0 >= 0 && ix0 >= 0 && iy0 + IH <= p.H && ix0 + IW <= p.W;
+    // (PP pieces, every one published: G::img_ops counts exactly these loads)
 #pragma unroll
-    for (int u = 0; u < PPM; ++u) {
-      int o = 0x7fffffe0;
-      if (u < PP) {
-        const Piece q = piece(u, std::integral_constant<int, last ? G::NSLL : 4>{});
-        o = (toff + (q.iy * p.W + q.ix) * p.xcs + q.slot * 8) * 4;
-        if (!inner) {
-          const int gy = iy0 + q.iy, gx = ix0 + q.ix;
-          if (!((unsigned)gy < (unsigned)p.H && (unsigned)gx < (unsigned)p.W)) o = 0x7fffffe0;
-        }
-        if ((u + 1) * NTH > NTOT && !q.valid) o = 0x7fffffe0;
+    for (int u = 0; u < PP; ++u) {
+      const Piece q = piece(u, std::integral_constant<int, last ? G::NSLL : 4>{});
+      int o = (toff + (q.iy * p.W + q.ix) * p.xcs + q.slot * 8) * 4;
+      if (!inner) {
+        const int gy = iy0 + q.iy, gx = ix0 + q.ix;
+        if (!((unsigned)gy < (unsigned)p.H && (unsigned)gx < (unsigned)p.W)) o = 0x7fffffe0;
       }
+      if ((u + 1) * NTH > NTOT && !q.valid) o = 0x7fffffe0;
       const f32x4 a = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, o, 0, 0));
       const f32x4 b = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, o + 16, 0, 0));
 #pragma unroll
@@ -721,6 +742,11 @@ xconv3_kernel(XP p) {
       // stage s: its weights (slot kw) and image (buffer q) are visible, its
       // operands are in register set S (read during the previous stage)
       constexpr int AH = G::AH, NSW = G::NSW;
+      // the ring slot and the image buffer of this stage: compile-time when
+      // the ring depth divides the stage count and a tile has an even number
+      // of chunks (the tile loop then returns both counters to 0)
+      const int kw_ = G::RING_STATIC ? s % NSW : kw;
+      const int q_ = CH % 2 == 0 ? (c & 1) : q;
       // per-stage opacity of the lane offsets: an address of this stage is
       // computed in it, never shared (CSE) with an equal one of a later stage
       // of the tile (the same tap of another chunk in the same image buffer,
@@ -728,7 +754,7 @@ xconv3_kernel(XP p) {
       opaque_v(aoff);
 #pragma unroll
       for (int dx = 0; dx < KS; ++dx) opaque_v(bo1[dx]), opaque_v(bo2[dx]);
-      const int wsa = kw + AH >= NSW ? kw + AH - NSW : kw + AH;
+      const int wsa = kw_ + AH >= NSW ? kw_ + AH - NSW : kw_ + AH;
       // 1-3: the stage's vector-memory work, in this order (vmcnt counts it):
       // 1. weights of stage s + AH (this tile or the next) into slot kw + AH;
       // 2. the next chunk's image pieces (first stage of a chunk);
@@ -751,10 +777,10 @@ xconv3_kernel(XP p) {
       if constexpr (!SPLITMF) issue_mem();
       // 4. operands of stage s + 1 into the other register set (the next
       // stage's weights landed and were published one barrier ago)
-      const int ws1 = kw + 1 >= NSW ? 0 : kw + 1;
+      const int ws1 = kw_ + 1 >= NSW ? 0 : kw_ + 1;
       constexpr int s1 = s + 1 < NST ? s + 1 : 0;
       constexpr int c1 = st_chunk<KT, CH>(s1);
-      const int ib1 = (s + 1 < NST ? (c1 == c ? q : q ^ 1) : q ^ 1);
+      const int ib1 = (s + 1 < NST ? (c1 == c ? q_ : q_ ^ 1) : q_ ^ 1);
       if constexpr (!late) {
         if constexpr (DBA)
           if (!(XDBG & 1)) read_a(std::integral_constant<int, S ^ 1>{}, ws1);
@@ -807,9 +833,9 @@ xconv3_kernel(XP p) {
         if constexpr (w0 >= 1) {
           if constexpr (rr >= w0 && rr <= pend)
             if (!(XDBG & 16))
-              publish(q ^ 1, CN{}, std::integral_constant<int, rr - w0>{}, std::integral_constant<int, rr - w0 + 1>{});
+              publish(q_ ^ 1, CN{}, std::integral_constant<int, rr - w0>{}, std::integral_constant<int, rr - w0 + 1>{});
         } else if constexpr (rr == pend) {
-          if (!(XDBG & 16)) publish(q ^ 1, CN{}, std::integral_constant<int, 0>{}, std::integral_constant<int, PPn>{});
+          if (!(XDBG & 16)) publish(q_ ^ 1, CN{}, std::integral_constant<int, 0>{}, std::integral_constant<int, PPn>{});
         }
       }
       // 7. epilogue

@@ -218,13 +218,15 @@ def test_xconv_7x7(case):
 
 
 @pytest.mark.parametrize("shape", ["48x48@1088x1920", "48x48@1088x1920r", "64x64@544x960r", "128x192@544x960u",
-                                   "96x48@1088x1920", "8x32@1088x1920k7"])
+                                   "96x48@1088x1920", "80x48@1088x1920", "8x32@1088x1920k7"])
 def test_xconv_repeated_launches_identical(shape):
     """The codec's dominant shapes launched again and again on fixed inputs:
     every launch bit-identical to sconv.hip's result.  A race in the weight
-    ring or the image buffers shows up here as an occasional mismatch (a
-    7-slot static ring variant of 48 -> 48 failed 10 of 40 launches this way
-    while passing every single-launch test; scripts/xconv_repeat.py)."""
+    ring or the image buffers shows up here as an occasional mismatch: with
+    the vmcnt count of a 16-channel last chunk's image loads 2 above the loads
+    hipcc kept, a 7-slot ring of 48 -> 48 failed 10-20 of 100 launches this
+    way while passing every single-launch test (scripts/xconv_repeat.py,
+    DESIGN.md section 9.0)."""
     import re
     h = K()
     m = re.fullmatch(r"(\d+)x(\d+)@(\d+)x(\d+)(k7)?(r*)(u?)", shape)
@@ -242,8 +244,8 @@ def test_xconv_repeated_launches_identical(shape):
     assert run(h, cw, x, ref, {"xconv": 0}, **kw).startswith("sconv_kernel")
     y = h.empty(H * f, W * f, co, h.F32)
     bad = 0
-    for _ in range(12):
+    for _ in range(20):
         y.buf.fill_(float("nan"))
         assert run(h, cw, x, y, {"xconv": 1}, **kw).startswith("xconv3_kernel")
         bad += int(not torch.equal(y.buf, ref.buf))
-    assert bad == 0, f"{bad} of 12 launches differ"
+    assert bad == 0, f"{bad} of 20 launches differ"
