@@ -585,6 +585,7 @@ extern "C" void dcvc_internal_sconv_resident(int v);
 extern "C" void dcvc_internal_sconv_res_waves(int v);
 extern "C" void dcvc_internal_sgemm_cfg(int v);
 extern "C" void dcvc_internal_sgemm_pd(int v);
+extern "C" void dcvc_internal_sgemm_gate(int v);
 extern "C" int dcvc_internal_set_option_split(const char *name, int value);
 extern "C" int dcvc_internal_xconv(const dcvc_conv_args *a, void *stream);
 extern "C" void dcvc_internal_xconv_enable(int v);
@@ -804,6 +805,10 @@ extern "C" int dcvc_set_option(const char *name, int value) {
   }
   if (std::strcmp(name, "sgemm_pd") == 0) {
     dcvc_internal_sgemm_pd(value);
+    return DCVC_HIP_OK;
+  }
+  if (std::strcmp(name, "sgemm_gate") == 0) {
+    dcvc_internal_sgemm_gate(value);
     return DCVC_HIP_OK;
   }
   if (std::strcmp(name, "sgemm") == 0) {

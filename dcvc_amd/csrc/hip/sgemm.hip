@@ -56,16 +56,17 @@ struct GP {
   int *ovf;               // fp16 range guard (split.h SplitRange)
 };
 
-template <int BN, int PXW, int PD>
+template <int BN, int PXW, int PD, bool GATE = false>
 struct GG {
   static constexpr int NT = BN / 16;
   static constexpr int BM = 4 * PXW * 16;
   static constexpr int NB = PD + 1;                 // LDS stage buffers
+  static constexpr int NX = GATE ? 2 : 1;           // pixel operands per stage: the values (and the gates)
   static constexpr int WH = BN * 64;                // halves of a stage's weights (hi rows, then lo rows)
-  static constexpr int XH = BM * 64;                // halves of a stage's pixels (fp32, 2 rows of 64 B per pixel)
+  static constexpr int XH = NX * BM * 64;           // halves of a stage's pixels (fp32, 2 rows of 64 B per pixel each)
   static constexpr int SH = WH + XH;                // halves of one stage buffer
   static constexpr int DPW = BN / 32;               // weight LDS-DMA pieces (1 KiB) per stage per wave
-  static constexpr int L = 2 * PXW + DPW;           // LDS-DMA instructions per stage per wave
+  static constexpr int L = 2 * NX * PXW + DPW;      // LDS-DMA instructions per stage per wave
   static constexpr size_t LDS = (size_t)NB * SH * 2 + 2 * BN * 4;
   static_assert(BN % 32 == 0, "BN must be a multiple of 32");
   static_assert((PD - 1) * L < 64, "vmcnt is 6 bits");
@@ -73,10 +74,10 @@ struct GG {
 
 constexpr int kOob = 0x7fffffe0;   // a buffer offset past any num_records: the load returns zeros
 
-template <int BN, int PXW, int PD>
+template <int BN, int PXW, int PD, bool GATE>
 __global__ void __launch_bounds__(256) sgemm_kernel(GP p) {
   SplitRange rg(p.ovf);
-  typedef GG<BN, PXW, PD> G_;
+  typedef GG<BN, PXW, PD, GATE> G_;
   constexpr int NT = G_::NT, BM = G_::BM, NB = G_::NB, WH = G_::WH, SH = G_::SH, DPW = G_::DPW, L = G_::L;
   extern __shared__ __align__(16) unsigned char smem[];
   uint16_t *Ls = reinterpret_cast<uint16_t *>(smem);
@@ -110,7 +111,8 @@ __global__ void __launch_bounds__(256) sgemm_kernel(GP p) {
   //   pixels:  per 16-pixel group r and channel half h, row h * 16 + px holds
   //            fp32 channels 16 h .. 16 h + 15 of the chunk (4 per slot).
   const int64_t eb = (int64_t)pix0 * p.xcs + p.xco;
-  int64_t nrec = ((int64_t)(p.npix - pix0 - 1) * p.xcs + p.cin) * 4;
+  // (gated input, ConvFFN2's second 1x1: 2 cin channels, the gates past the values)
+  int64_t nrec = ((int64_t)(p.npix - pix0 - 1) * p.xcs + (GATE ? 2 : 1) * p.cin) * 4;
   if (nrec > 0x7fff0000) nrec = 0x7fff0000;
   const __amdgpu_buffer_rsrc_t xr =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(p.x + eb), (short)0, (int)nrec, 0x00020000);
@@ -141,15 +143,17 @@ __global__ void __launch_bounds__(256) sgemm_kernel(GP p) {
           wr, (__attribute__((address_space(3))) void *)(Lb + hl * (WH / 2) + k * 512), 16, voff, 0, 0, 0);
     }
 #pragma unroll
-    for (int r = 0; r < PXW; ++r)
+    for (int gx = 0; gx < G_::NX; ++gx)
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int c = s * 32 + h * 16 + dls * 4;
-        const int o = (xoff[r] >= 0 && c < p.cin) ? xoff[r] + (s * 32 + h * 16) * 4 : kOob;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(
-            xr, (__attribute__((address_space(3))) void *)(Lb + WH + ((wave * PXW + r) * 2 + h) * 512), 16, o, 0, 0,
-            0);
-      }
+      for (int r = 0; r < PXW; ++r)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int c = s * 32 + h * 16 + dls * 4;
+          const int o = (xoff[r] >= 0 && c < p.cin) ? xoff[r] + (s * 32 + h * 16 + gx * p.cin) * 4 : kOob;
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(
+              xr, (__attribute__((address_space(3))) void *)(Lb + WH + gx * (BM * 64) + ((wave * PXW + r) * 2 + h) * 512),
+              16, o, 0, 0, 0);
+        }
   };
 
   f32x4 am[PXW][NT], ac[PXW][NT];
@@ -186,7 +190,19 @@ __global__ void __launch_bounds__(256) sgemm_kernel(GP p) {
         v[e] = a[e];
         v[4 + e] = c[e];
       }
-      if (lrelu) {
+      if constexpr (GATE) {
+        // x1 * lrelu(x2) (sconv.hip's gate, same order)
+        const uint16_t *grow = xrow + BM * 64;
+        const f32x4 ga = *reinterpret_cast<const f32x4 *>(grow + swz(col, (hi & 1) * 2));
+        const f32x4 gc = *reinterpret_cast<const f32x4 *>(grow + swz(col, (hi & 1) * 2 + 1));
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float g0 = ga[e] >= 0.f ? ga[e] : ga[e] * p.in_slope;
+          const float g1 = gc[e] >= 0.f ? gc[e] : gc[e] * p.in_slope;
+          v[e] = v[e] * g0;
+          v[4 + e] = v[4 + e] * g1;
+        }
+      } else if (lrelu) {
 #pragma unroll
         for (int e = 0; e < 8; ++e) v[e] = v[e] >= 0.f ? v[e] : v[e] * p.in_slope;
       }
@@ -293,17 +309,18 @@ int64_t tiles_of(const GP &p) {
   return (int64_t)((p.npix + 64 * PXW - 1) / (64 * PXW)) * ((p.cout + BN - 1) / BN);
 }
 
-template <int BN, int PXW, int PD>
+template <int BN, int PXW, int PD, bool GATE = false>
 int launch(GP p, hipStream_t st) {
-  typedef GG<BN, PXW, PD> G_;
+  typedef GG<BN, PXW, PD, GATE> G_;
   p.nblk = (p.cout + BN - 1) / BN;
   const int64_t nt = tiles_of<BN, PXW>(p);
   if (nt <= 0) return DCVC_HIP_OK;
   if (nt > 0x7fffffff) return DCVC_HIP_EINVAL;
   p.ntiles = (int)nt;
-  auto kern = sgemm_kernel<BN, PXW, PD>;
+  auto kern = sgemm_kernel<BN, PXW, PD, GATE>;
   if (G_::LDS > 160 * 1024) return DCVC_HIP_EUNSUPPORTED;
-  dcvc_note_kernel("sgemm_kernel<%d, %d, %d>", BN, PXW, PD);
+  if (GATE) dcvc_note_kernel("sgemm_kernel<%d, %d, %d, true>", BN, PXW, PD);
+  else dcvc_note_kernel("sgemm_kernel<%d, %d, %d>", BN, PXW, PD);
   dcvc_ensure_lds(reinterpret_cast<const void *>(kern), (int)G_::LDS);
   hipLaunchKernelGGL(kern, dim3((unsigned)nt), dim3(256), G_::LDS, st, p);
   DCVC_LAUNCH_CHECK();
@@ -315,6 +332,9 @@ int launch(GP p, hipStream_t st) {
 int g_cfg = 0;
 int g_cus = 0;
 int g_pd = 0;   // dcvc_set_option("sgemm_pd", 1 | 2 | 3 | 5): stages in flight (A/B); 0 = auto
+// dcvc_set_option("sgemm_gate", 0): ConvFFN2's gated 1x1 below dconv.hip's
+// pixel count back to sconv.hip (A/B)
+int g_gate = 1;
 
 template <int PD>
 int run_pd(int cfg, const GP &p, hipStream_t st) {
@@ -333,7 +353,20 @@ int run_pd(int cfg, const GP &p, hipStream_t st) {
 // and epilogue better than a deeper ring: measured on the codec's 1x1 layers
 // (scripts/gpu_r03za.sh), 384 -> 384 at 68x120 25.5 -> 17.7 us, 96 -> 48 at
 // 1080p 394 -> 272 us, 128 -> 64 at 544x960 148 -> 120 us
+// gated input: the auto depth only
+int run_gate(int cfg, const GP &p, hipStream_t st) {
+  switch (cfg) {
+    case 1: return launch<128, 2, 2, true>(p, st);
+    case 2: return launch<64, 2, 2, true>(p, st);
+    case 3: return launch<32, 2, 2, true>(p, st);
+    case 4: return launch<128, 1, 2, true>(p, st);
+    case 5: return launch<64, 1, 2, true>(p, st);
+    case 6: return launch<32, 1, 2, true>(p, st);
+    default: return DCVC_HIP_EUNSUPPORTED;
+  }
+}
 int run_cfg(int cfg, const GP &p, hipStream_t st) {
+  if (p.in_op == DCVC_IN_GATE) return run_gate(cfg, p, st);
   const int pd = g_pd ? g_pd : 2;
   if (pd == 1) return run_pd<1>(cfg, p, st);
   if (pd == 2) return run_pd<2>(cfg, p, st);
@@ -345,14 +378,17 @@ int run_cfg(int cfg, const GP &p, hipStream_t st) {
 
 extern "C" void dcvc_internal_sgemm_cfg(int v) { g_cfg = v; }
 extern "C" void dcvc_internal_sgemm_pd(int v) { g_pd = v; }
+extern "C" void dcvc_internal_sgemm_gate(int v) { g_gate = v; }
 
 // The f16x3 1x1 stride-1 convolutions sconv.hip hands over (no pad, no pixel
-// shuffle, no gate, 8-channel aligned input, 4-channel aligned output pieces);
+// shuffle with a gate, 8-channel aligned input, 4-channel aligned output pieces);
 // DCVC_HIP_EUNSUPPORTED sends the call back to sconv.hip.
 extern "C" int dcvc_internal_sgemm(const dcvc_conv_args *a, void *stream) {
   if (g_cfg < 0) return DCVC_HIP_EUNSUPPORTED;
   if (a->kh != 1 || a->kw != 1 || a->stride != 1 || a->pad != 0) return DCVC_HIP_EUNSUPPORTED;
-  if (a->in_op != DCVC_IN_NONE && a->in_op != DCVC_IN_LRELU) return DCVC_HIP_EUNSUPPORTED;
+  const bool gate = a->in_op == DCVC_IN_GATE;
+  if (a->in_op != DCVC_IN_NONE && a->in_op != DCVC_IN_LRELU && !(gate && g_gate)) return DCVC_HIP_EUNSUPPORTED;
+  if (gate && a->shuffle) return DCVC_HIP_EUNSUPPORTED;
   if (a->x.dtype != DCVC_F32 || a->y.dtype != DCVC_F32) return DCVC_HIP_EUNSUPPORTED;
   const int f = a->shuffle ? 2 : 1;
   if (a->x.H * f != a->y.H || a->x.W * f != a->y.W) return DCVC_HIP_EUNSUPPORTED;

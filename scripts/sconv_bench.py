@@ -3,7 +3,8 @@
     python scripts/sconv_bench.py [--reps 20] [--shapes 48x48@1088x1920k3r,...] [--opt NAME=VALUE]
 
 A shape is CINxCOUT@HxW then kK (kernel size, default 3), sS (stride,
-default 1), "r" for an fp32 residual input and "u" for a pixel-shuffled output.  One JSON line per shape:
+default 1), "r" for an fp32 residual input, "u" for a pixel-shuffled output and "g" for a
+ConvFFN2-gated input (2 CIN channels, x1 * lrelu(x2)).  One JSON line per shape:
 kernel, us/launch, algorithmic GB/s (fp32 input, split weights, output,
 residual once each) and fp32-equivalent TFLOP/s (against 2500/3 = 833 peak).
 """
@@ -36,27 +37,29 @@ def main():
         if name != "arm":   # (a label only: which library of an A/B run)
             K.set_option(name, int(val))
     for sh in a.shapes.split(","):
-        m = re.fullmatch(r"(\d+)x(\d+)@(\d+)x(\d+)(?:k(\d))?(?:s(\d))?(r?)(u?)", sh)
+        m = re.fullmatch(r"(\d+)x(\d+)@(\d+)x(\d+)(?:k(\d))?(?:s(\d))?(r?)(u?)(g?)", sh)
         cin, cout, H, W = (int(m.group(i)) for i in range(1, 5))
         k = int(m.group(5) or 3)
         s = int(m.group(6) or 1)
         res = m.group(7) == "r"
         shuf = m.group(8) == "u"
+        gate = m.group(9) == "g"
+        gk = dict(in_op=K.IN_GATE, in_slope=0.1) if gate else {}
         cw = K.ConvW(torch.randn(cout, cin, k, k) / (cin * k * k) ** 0.5, torch.randn(cout) * 0.1, s, K.F16X3, dev)
-        x = K.from_nchw(torch.randn(1, cin, H, W, device=dev), K.F32)
+        x = K.from_nchw(torch.randn(1, 2 * cin if gate else cin, H, W, device=dev), K.F32)
         Ho, Wo = cw.out_hw(H, W)
         r = K.from_nchw(torch.randn(1, cout, Ho, Wo, device=dev), K.F32) if res else None
         y = K.empty(Ho * 2, Wo * 2, cout // 4, K.F32, dev) if shuf else K.empty(Ho, Wo, cout, K.F32, dev)
         for _ in range(3):
-            K.conv(cw, x, y, act=K.ACT_LRELU, slope=0.1, res=r, shuffle=shuf)
+            K.conv(cw, x, y, act=K.ACT_LRELU, slope=0.1, res=r, shuffle=shuf, **gk)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         for _ in range(a.reps):
-            K.conv(cw, x, y, act=K.ACT_LRELU, slope=0.1, res=r, shuffle=shuf)
+            K.conv(cw, x, y, act=K.ACT_LRELU, slope=0.1, res=r, shuffle=shuf, **gk)
         e1.record()
         torch.cuda.synchronize()
         us = e0.elapsed_time(e1) * 1e3 / a.reps
-        nb = 4 * (H * W * cin + Ho * Wo * cout * (2 if res else 1)) + cw.w.numel() * 2
+        nb = 4 * (H * W * cin * (2 if gate else 1) + Ho * Wo * cout * (2 if res else 1)) + cw.w.numel() * 2
         fl = 2.0 * Ho * Wo * cin * cout * k * k
         print(json.dumps({"shape": sh, "opt": a.opt, "kernel": K.lib().dcvc_last_kernel().decode(), "us": round(us, 2),
                           "gbs": round(nb / us / 1e3, 1), "tflops": round(fl / us / 1e6, 1),

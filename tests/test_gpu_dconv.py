@@ -198,13 +198,49 @@ def test_dconv_gated_1x1_matches_sconv(cin, cout, H, W):
     outs = []
     for on in (1, 0):
         h.set_option("dconv", on)
+        h.set_option("sgemm_gate", on)
         try:
             y = h.conv(cw, xa, out_dtype=h.F32, in_op=h.IN_GATE, in_slope=0.1, res=ra)
             torch.cuda.synchronize()
             kern = h.lib().dcvc_last_kernel().decode()
         finally:
             h.set_option("dconv", 1)
+            h.set_option("sgemm_gate", 1)
         assert (kern.startswith("dconv_kernel<1") and ", true>" in kern) if on else kern.startswith("sconv_kernel"), kern
+        outs.append(y.nchw().cpu())
+    assert rel_err(outs[0], ref) < TOL
+    assert torch.equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("cin,cout,H,W", [(512, 256, 68, 120), (1536, 768, 68, 120), (1024, 512, 68, 120),
+                                          (512, 256, 136, 240), (256, 128, 34, 60), (96, 40, 17, 23)])
+def test_sgemm_gated_1x1_matches_sconv(cin, cout, H, W):
+    """The intra codec's latent-rate ConvFFN2 gated 1x1s (DCVC-DC
+    image_model.py:62-91 DepthConvBlock2 at 1/16 and 1/8 scale, layers.py:182-
+    197), below dconv.hip's pixel count: the pixel-GEMM kernel with the gate
+    applied to its DMA-staged operand, against sconv.hip's gated path bit for
+    bit (same K order and gate order) and fp64; a ragged last pixel block."""
+    h = K()
+    g = torch.Generator().manual_seed(cin + cout + H)
+    x = torch.randn(1, 2 * cin, H, W, generator=g)
+    w = torch.randn(cout, cin, 1, 1, generator=g) / cin ** 0.5
+    b = torch.randn(cout, generator=g) * 0.1
+    r = torch.randn(1, cout, H, W, generator=g)
+    xd = x.double()
+    gated = xd[:, :cin] * F.leaky_relu(xd[:, cin:], 0.1)
+    ref = r.double() + F.conv2d(gated, w.double(), b.double())
+    cw = h.ConvW(w, b, 1, h.F16X3)
+    xa, ra = h.from_nchw(x, h.F32), h.from_nchw(r, h.F32)
+    outs = []
+    for on in (1, 0):
+        h.set_option("sgemm_gate", on)
+        try:
+            y = h.conv(cw, xa, out_dtype=h.F32, in_op=h.IN_GATE, in_slope=0.1, res=ra)
+            torch.cuda.synchronize()
+            kern = h.lib().dcvc_last_kernel().decode()
+        finally:
+            h.set_option("sgemm_gate", 1)
+        assert (kern.startswith("sgemm_kernel") and ", true>" in kern) if on else kern.startswith("sconv_kernel"), kern
         outs.append(y.nchw().cpu())
     assert rel_err(outs[0], ref) < TOL
     assert torch.equal(outs[0], outs[1])
