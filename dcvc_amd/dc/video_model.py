@@ -42,6 +42,30 @@ def dpb_in(dpb):
     return {k: (as_act(v) if isinstance(v, torch.Tensor) else v) for k, v in dpb.items()}
 
 
+class Contexts:
+    """The three contexts of MultiScaleContextFusion (video_model.py:103-118),
+    each written by its producer straight into the concatenation its consumers
+    read, so no context is copied into a concat buffer:
+      b1 = cat(cd_up4 out (32), c1 (48), x (3), 0 x5) at full size: the
+           contextual encoder reads channels 32..87 (its cat(c1, x, 0 x5)),
+           the reconstruction channels 0..79 (cat(up4, c1));
+      b2 = cat(first conv out, c2) at 1/2, b3 = cat(first conv out, c3) at 1/4:
+           the encoder (video_model.py:173-195) and the reconstruction
+           (:197-232) each write the first half, one after the other on the
+           frame's stream, and read the context in the second.
+    b1's pad channels stay zero (a cached buffer, allocated zeroed)."""
+
+    def __init__(self, net, H, W):
+        feat, dev = net.prec.feat, net.dev
+        self.b1 = net._padded("ctx1", H, W, 32 + G1 + 8)
+        self.b2 = K.empty(H // 2, W // 2, G2 + G2, feat, dev)
+        self.b3 = K.empty(H // 4, W // 4, G4 + G4, feat, dev)
+        self.c1, self.c2, self.c3 = self.b1.ch(32, G1), self.b2.ch(G2, G2), self.b3.ch(G4, G4)
+
+    def __iter__(self):   # c1, c2, c3 = ctx (diagnostics that checksum the contexts)
+        return iter((self.c1, self.c2, self.c3))
+
+
 class DMC:
     def __init__(self, anchor_num=4, ec_thread=False, stream_part=1, inplace=False, precision=None,
                  device=None):
@@ -271,46 +295,35 @@ class DMC:
         cat2 = K.empty(H // 2, W // 2, G2 + G2, feat, dev)             # cat(c3_up, c2)
         c2 = K.flow_warp(r2, mv2, self.grids(H // 2, W // 2), y=cat2.ch(G2, G2))
         c3 = K.flow_warp(r3, mv3, self.grids(H // 4, W // 4))
-        # MultiScaleContextFusion (video_model.py:103-118)
+        # MultiScaleContextFusion (video_model.py:103-118), each context
+        # written straight into the concat buffers its consumers read (Contexts)
+        ctx = Contexts(self, H, W)
         self.cf_r3up(K.conv(self.cf_c3up, c3, shuffle=True), y=cat2.ch(0, G2))
-        context3 = self.cf_r3out(K.conv(self.cf_c3out, c3), res2=c3)
+        self.cf_r3out(K.conv(self.cf_c3out, c3), res2=c3, y=ctx.c3)
         self.cf_r2up(K.conv(self.cf_c2up, cat2, shuffle=True), y=cat1.ch(0, G1))
-        context2 = self.cf_r2out(K.conv(self.cf_c2out, cat2), res2=c2)
-        context1 = self.cf_r1out(K.conv(self.cf_c1out, cat1), res2=c1)
-        return context1, context2, context3
+        self.cf_r2out(K.conv(self.cf_c2out, cat2), res2=c2, y=ctx.c2)
+        self.cf_r1out(K.conv(self.cf_c1out, cat1), res2=c1, y=ctx.c1)
+        return ctx
 
-    def _contextual_encoder(self, x, c1, c2, c3, q):
-        feat, dev = self.prec.feat, self.dev
-        cat = self._padded("ce", x.H, x.W, 56)                         # cat(c1, x, 0 x5)
-        K.copy(c1, cat.ch(0, G1))
-        K.copy(x, cat.ch(G1, 3))
-        cat2 = K.empty(c2.H, c2.W, G2 + G2, feat, dev)
-        K.conv(self.ce_c1, cat, cat2.ch(0, G2))
-        K.copy(c2, cat2.ch(G2, G2))
-        f = self.ce_r1(cat2, scale=q)
-        cat3 = K.empty(c3.H, c3.W, G4 + G4, feat, dev)
-        K.conv(self.ce_c2, f, cat3.ch(0, G4))
-        K.copy(c3, cat3.ch(G4, G4))
-        f = self.ce_r2(cat3)
+    def _contextual_encoder(self, x, ctx, q):
+        K.copy(x, ctx.b1.ch(32 + G1, 3))
+        K.conv(self.ce_c1, ctx.b1.ch(32, 56), ctx.b2.ch(0, G2))       # cat(c1, x, 0 x5)
+        f = self.ce_r1(ctx.b2, scale=q)                                # cat(., c2)
+        K.conv(self.ce_c2, f, ctx.b3.ch(0, G4))
+        f = self.ce_r2(ctx.b3)                                         # cat(., c3)
         f = K.conv(self.ce_c3, f)
         return K.conv(self.ce_c4, f, out_dtype=F32)
 
-    def _recon(self, y_hat, c1, c2, c3, q):
+    def _recon(self, y_hat, ctx, q):
         """get_recon_and_feature (video_model.py:401-405)."""
-        feat, dev = self.prec.feat, self.dev
+        feat = self.prec.feat
         f = K.conv(self.cd_up1, y_hat, out_dtype=feat, shuffle=True)
-        cat3 = K.empty(c3.H, c3.W, G4 + G4, feat, dev)
-        K.conv(self.cd_up2, f, cat3.ch(0, G4), shuffle=True)
-        K.copy(c3, cat3.ch(G4, G4))
-        f = self.cd_r1(cat3)
-        cat2 = K.empty(c2.H, c2.W, G2 + G2, feat, dev)
-        K.conv(self.cd_up3, f, cat2.ch(0, G2), shuffle=True, scale=q)
-        K.copy(c2, cat2.ch(G2, G2))
-        f = self.cd_r2(cat2)
-        cat1 = K.empty(c1.H, c1.W, 32 + G1, feat, dev)
-        K.conv(self.cd_up4, f, cat1.ch(0, 32), shuffle=True)
-        K.copy(c1, cat1.ch(32, G1))
-        f = K.conv(self.rg_first, cat1)
+        K.conv(self.cd_up2, f, ctx.b3.ch(0, G4), shuffle=True)
+        f = self.cd_r1(ctx.b3)                                         # cat(., c3)
+        K.conv(self.cd_up3, f, ctx.b2.ch(0, G2), shuffle=True, scale=q)
+        f = self.cd_r2(ctx.b2)                                         # cat(., c2)
+        K.conv(self.cd_up4, f, ctx.b1.ch(0, 32), shuffle=True)
+        f = K.conv(self.rg_first, ctx.b1.ch(0, 32 + G1))              # cat(., c1)
         f = self.rg_u1(f)
         feature = self.rg_u2(f)
         x_hat = K.conv(self.rg_out, feature, out_dtype=F32, act=ACT_CLAMP01)
@@ -341,11 +354,11 @@ class DMC:
         K.to_symbols(mv_z_hat, sb.sym_slice(c_mvz))
         mv_y_hat = self.mv_prior.encode(mv_y, mv_params, sb, c_mv, self.scale_table)
         mv_hat, _ = self._mv_decoder(mv_y_hat, mv_q_dec)
-        c1, c2, c3 = self._motion_compensation(dpb, mv_hat, frame_idx)
-        y = self._contextual_encoder(x, c1, c2, c3, y_q_enc)
+        ctx = self._motion_compensation(dpb, mv_hat, frame_idx)
+        y = self._contextual_encoder(x, ctx, y_q_enc)
         z_hat = self.y_henc(pad_for_y(y))
         K.to_symbols(z_hat, sb.sym_slice(c_z))
-        params = self._res_prior_params(z_hat, dpb, c3, yh, yw)
+        params = self._res_prior_params(z_hat, dpb, ctx.c3, yh, yw)
         self.y_prior.encode(y, params, sb, c_y, self.scale_table)
         host = sb.to_host()
 
@@ -382,10 +395,10 @@ class DMC:
         mv_params = self._mv_prior_params(mv_z_hat, dpb, yh, yw)
         mv_y_hat = self.mv_prior.decode(mv_params, dec, self.scale_table)
         mv_hat, mv_feature = self._mv_decoder(mv_y_hat, mv_q_dec)
-        c1, c2, c3 = self._motion_compensation(dpb, mv_hat, frame_idx)
-        params = self._res_prior_params(z_hat, dpb, c3, yh, yw)
+        ctx = self._motion_compensation(dpb, mv_hat, frame_idx)
+        params = self._res_prior_params(z_hat, dpb, ctx.c3, yh, yw)
         y_hat = self.y_prior.decode(params, dec, self.scale_table)
-        x_hat, feature = self._recon(y_hat, c1, c2, c3, y_q_dec)
+        x_hat, feature = self._recon(y_hat, ctx, y_q_dec)
         return {"dpb": {"ref_frame": x_hat.nchw_view(), "ref_feature": feature, "ref_mv_feature": mv_feature,
                         "ref_y": y_hat, "ref_mv_y": mv_y_hat}}
 
@@ -407,13 +420,13 @@ class DMC:
         mv_params = self._mv_prior_params(mv_z_hat, dpb, yh, yw)
         mv_y_hat = self.mv_prior.estimate(mv_y, mv_params, bc.buffer("mv_y", 64 * yh * yw), False)
         mv_hat, mv_feature = self._mv_decoder(mv_y_hat, mv_q_dec)
-        c1, c2, c3 = self._motion_compensation(dpb, mv_hat, frame_idx)
-        y = self._contextual_encoder(x, c1, c2, c3, y_q_enc)
+        ctx = self._motion_compensation(dpb, mv_hat, frame_idx)
+        y = self._contextual_encoder(x, ctx, y_q_enc)
         z_hat = self.y_henc(pad_for_y(y))
         bc.factorized("z", z_hat, self.z_table)
-        params = self._res_prior_params(z_hat, dpb, c3, yh, yw)
+        params = self._res_prior_params(z_hat, dpb, ctx.c3, yh, yw)
         y_hat = self.y_prior.estimate(y, params, bc.buffer("y", G16 * yh * yw), False)
-        x_hat, feature = self._recon(y_hat, c1, c2, c3, y_q_dec)
+        x_hat, feature = self._recon(y_hat, ctx, y_q_dec)
         out = bits_result(bc.totals(), x.H * x.W, ("mv_y", "mv_z", "y", "z"))
         out["dpb"] = {"ref_frame": x_hat.nchw_view(), "ref_feature": feature, "ref_mv_feature": mv_feature,
                       "ref_y": y_hat, "ref_mv_y": mv_y_hat}

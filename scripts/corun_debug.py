@@ -74,7 +74,9 @@ def main():
                 else:
                     rec(f"{m} in[{j}]", v)
             out = f(*a, **kw)
-            for j, o in enumerate(out if isinstance(out, tuple) else (out,)):
+            outs = tuple(out) if isinstance(out, tuple) or hasattr(out, "__iter__") and not hasattr(out, "buf") \
+                and not isinstance(out, (dict, torch.Tensor)) else (out,)
+            for j, o in enumerate(outs):
                 rec(f"{m} out[{j}]", o)
             return out
         setattr(obj, m, wrapped)

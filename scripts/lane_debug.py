@@ -65,7 +65,8 @@ def main():
                     tl.in_mc = _m == "_motion_compensation"
                     out = _f(*a, **kw)
                     tl.in_mc = False
-                    for j, o in enumerate(out if isinstance(out, tuple) else (out,)):
+                    outs = out if isinstance(out, tuple) else tuple(out) if type(out).__name__ == "Contexts" else (out,)
+                    for j, o in enumerate(outs):
                         rec(f"{_m}[{j}]", o)
                     return out
                 setattr(p, m, wrapped)
