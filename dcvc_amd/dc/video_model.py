@@ -55,12 +55,13 @@ class Contexts:
            frame's stream, and read the context in the second.
     b1's pad channels stay zero (a cached buffer, allocated zeroed)."""
 
-    def __init__(self, net, H, W):
+    def __init__(self, net, H, W, C1=G1, C2=G2, C3=G4):
+        # (DCVC-HEM: 64 channels at every scale, its encoder's cat(c1, x, 0 x5) is 72 wide)
         feat, dev = net.prec.feat, net.dev
-        self.b1 = net._padded("ctx1", H, W, 32 + G1 + 8)
-        self.b2 = K.empty(H // 2, W // 2, G2 + G2, feat, dev)
-        self.b3 = K.empty(H // 4, W // 4, G4 + G4, feat, dev)
-        self.c1, self.c2, self.c3 = self.b1.ch(32, G1), self.b2.ch(G2, G2), self.b3.ch(G4, G4)
+        self.b1 = net._padded("ctx1", H, W, 32 + C1 + 8)
+        self.b2 = K.empty(H // 2, W // 2, 2 * C2, feat, dev)
+        self.b3 = K.empty(H // 4, W // 4, 2 * C3, feat, dev)
+        self.c1, self.c2, self.c3 = self.b1.ch(32, C1), self.b2.ch(C2, C2), self.b3.ch(C3, C3)
 
     def __iter__(self):   # c1, c2, c3 = ctx (diagnostics that checksum the contexts)
         return iter((self.c1, self.c2, self.c3))

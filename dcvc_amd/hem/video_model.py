@@ -19,7 +19,7 @@ from ..layers import split_guarded, split_checkpoint, Ctx, Precision, SpyNet, Gr
 from ..entropy import ScaleTable, FactorizedTable
 from ..stream_helper import get_downsampled_shape, filesize, get_state_dict
 from ..dc.common import SymbolBuffer, BitCounter, bits_result
-from ..dc.video_model import as_act, dpb_in
+from ..dc.video_model import as_act, dpb_in, Contexts
 from .common import DualPrior, HemEntropyCoder, lower_bound_q, get_rounded_q
 from .layers import ResBlock, EncTower, DecTower, UNet, Seq3, chunk3_to_buffer_order
 from .stream_helper import encode_p, decode_p
@@ -178,47 +178,36 @@ class DMC:
         cat2 = K.empty(H // 2, W // 2, 2 * CH_N, feat, dev)            # cat(context3_up, context2)
         c2 = K.flow_warp(l2, mv2, self.grids(H // 2, W // 2), y=cat2.ch(CH_N, CH_N))
         c3 = K.flow_warp(l3, mv3, self.grids(H // 4, W // 4))
+        # each context written straight into the concat buffers its consumers
+        # read (dc.video_model.Contexts: b1 = cat(up4 (32), c1, x, 0 x5))
+        ctx = Contexts(self, H, W, CH_N, CH_N, CH_N)
         self.cf_r3up(K.conv(self.cf_c3up, c3, shuffle=True), y=cat2.ch(0, CH_N))
-        context3 = self.cf_r3out(K.conv(self.cf_c3out, c3), res2=c3)
+        self.cf_r3out(K.conv(self.cf_c3out, c3), res2=c3, y=ctx.c3)
         self.cf_r2up(K.conv(self.cf_c2up, cat2, shuffle=True), y=cat1.ch(0, CH_N))
-        context2 = self.cf_r2out(K.conv(self.cf_c2out, cat2), res2=c2)
-        context1 = self.cf_r1out(K.conv(self.cf_c1out, cat1), res2=c1)
-        return context1, context2, context3
+        self.cf_r2out(K.conv(self.cf_c2out, cat2), res2=c2, y=ctx.c2)
+        self.cf_r1out(K.conv(self.cf_c1out, cat1), res2=c1, y=ctx.c1)
+        return ctx
 
-    def _contextual_encoder(self, x, c1, c2, c3, yq):
+    def _contextual_encoder(self, x, ctx, yq):
         """ContextualEncoder (:71-95), then y / curr_y_q."""
-        feat, dev = self.prec.feat, self.dev
-        cat = self._padded("ce", x.H, x.W, 72)                          # cat(context1, x, 0 x5)
-        K.copy(c1, cat.ch(0, CH_N))
-        K.copy(x, cat.ch(CH_N, 3))
-        cat2 = K.empty(c2.H, c2.W, 2 * CH_N, feat, dev)
-        K.conv(self.ce_c1, cat, cat2.ch(0, CH_N))
-        K.copy(c2, cat2.ch(CH_N, CH_N))
-        f = self.ce_r1(cat2)
-        cat3 = K.empty(c3.H, c3.W, 2 * CH_N, feat, dev)
-        K.conv(self.ce_c2, f, cat3.ch(0, CH_N))
-        K.copy(c3, cat3.ch(CH_N, CH_N))
-        f = self.ce_r2(cat3)
+        K.copy(x, ctx.b1.ch(32 + CH_N, 3))
+        K.conv(self.ce_c1, ctx.b1.ch(32, 72), ctx.b2.ch(0, CH_N))     # cat(context1, x, 0 x5)
+        f = self.ce_r1(ctx.b2)                                         # cat(., context2)
+        K.conv(self.ce_c2, f, ctx.b3.ch(0, CH_N))
+        f = self.ce_r2(ctx.b3)                                         # cat(., context3)
         f = K.conv(self.ce_c3, f)
         y = K.conv(self.ce_c4, f, out_dtype=F32)
         return K.channel_div(y, yq, y)
 
-    def _recon(self, y_hat, c1, c2, c3, clamp=True):
+    def _recon(self, y_hat, ctx, clamp=True):
         """ContextualDecoder + ReconGeneration (:98-128)."""
-        feat, dev = self.prec.feat, self.dev
-        f = K.conv(self.cd_up1, y_hat, out_dtype=feat, shuffle=True)
-        cat3 = K.empty(c3.H, c3.W, 2 * CH_N, feat, dev)
-        K.conv(self.cd_up2, f, cat3.ch(0, CH_N), shuffle=True)
-        K.copy(c3, cat3.ch(CH_N, CH_N))
-        f = self.cd_r1(cat3)
-        cat2 = K.empty(c2.H, c2.W, 2 * CH_N, feat, dev)
-        K.conv(self.cd_up3, f, cat2.ch(0, CH_N), shuffle=True)
-        K.copy(c2, cat2.ch(CH_N, CH_N))
-        f = self.cd_r2(cat2)
-        cat1 = K.empty(c1.H, c1.W, 32 + CH_N, feat, dev)
-        K.conv(self.cd_up4, f, cat1.ch(0, 32), shuffle=True)
-        K.copy(c1, cat1.ch(32, CH_N))
-        f = K.conv(self.rg_first, cat1)
+        f = K.conv(self.cd_up1, y_hat, out_dtype=self.prec.feat, shuffle=True)
+        K.conv(self.cd_up2, f, ctx.b3.ch(0, CH_N), shuffle=True)
+        f = self.cd_r1(ctx.b3)                                         # cat(., context3)
+        K.conv(self.cd_up3, f, ctx.b2.ch(0, CH_N), shuffle=True)
+        f = self.cd_r2(ctx.b2)                                         # cat(., context2)
+        K.conv(self.cd_up4, f, ctx.b1.ch(0, 32), shuffle=True)
+        f = K.conv(self.rg_first, ctx.b1.ch(0, 32 + CH_N))            # cat(., context1)
         f = self.rg_u1(f)
         feature = self.rg_u2(f)
         x_hat = K.conv(self.rg_out, feature, out_dtype=F32, act=ACT_CLAMP01 if clamp else K.ACT_NONE)
@@ -237,14 +226,14 @@ class DMC:
         mv_buf = self._mv_params(mv_z_hat, dpb["ref_mv_y"], yh, yw)
         mv_y_hat = mv_prior_fn(mv_y, mv_buf)
         mv_hat = self.mv_dec(mv_y_hat, out_dtype=F32)
-        c1, c2, c3 = self._motion_compensation(dpb, mv_hat)
-        y = self._contextual_encoder(x, c1, c2, c3, yq)
+        ctx = self._motion_compensation(dpb, mv_hat)
+        y = self._contextual_encoder(x, ctx, yq)
         z_hat = self.y_henc(y)
         if bc is not None:
             bc.factorized("z", z_hat, self.z_table)
-        buf = self._y_params(z_hat, c3, dpb["ref_y"], yh, yw)
+        buf = self._y_params(z_hat, ctx.c3, dpb["ref_y"], yh, yw)
         y_hat = y_prior_fn(y, buf)
-        return mv_z_hat, mv_y_hat, z_hat, y_hat, (c1, c2, c3)
+        return mv_z_hat, mv_y_hat, z_hat, y_hat, ctx
 
     # --------------------------------------------------------------- codec
     def compress(self, x, dpb, mv_y_q_scale, y_q_scale):
@@ -301,13 +290,13 @@ class DMC:
         mv_buf = self._mv_params(mv_z_hat, dpb["ref_mv_y"], yh, yw)
         mv_y_hat = self.mv_prior.decode(mv_buf, mvq, dec, st)
         mv_hat = self.mv_dec(mv_y_hat, out_dtype=F32)
-        c1, c2, c3 = self._motion_compensation(dpb, mv_hat)
+        ctx = self._motion_compensation(dpb, mv_hat)
         z = ec.decode(self.z_table.indexes(zh, zw).astype("int32"), self.z_table.table)
         z_hat = K.empty(zh, zw, CH_N, F32, dev)
         K.from_symbols_i32(K.upload(z, dev, "z"), z_hat)
-        buf = self._y_params(z_hat, c3, dpb["ref_y"], yh, yw)
+        buf = self._y_params(z_hat, ctx.c3, dpb["ref_y"], yh, yw)
         y_hat = self.y_prior.decode(buf, yq, dec, st)
-        x_hat, feature = self._recon(y_hat, c1, c2, c3)
+        x_hat, feature = self._recon(y_hat, ctx)
         return {"dpb": {"ref_frame": x_hat.nchw_view(), "ref_feature": feature, "ref_y": y_hat,
                         "ref_mv_y": mv_y_hat}}
 
@@ -327,8 +316,8 @@ class DMC:
 
         def y_prior(y, buf):
             return self.y_prior.estimate(y, buf, yq, bc.buffer("y", CH_M * yh * yw), False)
-        _, mv_y_hat, _, y_hat, (c1, c2, c3) = self._analysis(x, dpb, mvq, yq, mv_prior, y_prior, bc)
-        x_hat, feature = self._recon(y_hat, c1, c2, c3, clamp=False)
+        _, mv_y_hat, _, y_hat, ctx = self._analysis(x, dpb, mvq, yq, mv_prior, y_prior, bc)
+        x_hat, feature = self._recon(y_hat, ctx, clamp=False)
         out = bits_result(bc.totals(), H * W, ("mv_y", "mv_z", "y", "z"))
         out["dpb"] = {"ref_frame": x_hat.nchw_view(), "ref_feature": feature, "ref_y": y_hat, "ref_mv_y": mv_y_hat}
         return out
