@@ -15,8 +15,10 @@
 //   stage = one K step of 32 (one tap of a 32-channel chunk, or 2 / 4 packed
 //           taps of a 16- / 8-channel last chunk), one workgroup barrier;
 //   weights: streamed through a ring of LDS slots by LDS-DMA, issued as many
-//           stages ahead as the ring is deep (8 to 12 slots; L2-resident:
-//           every tile reads the same weights);
+//           stages ahead as the ring is deep (6 to 12 slots, a depth that
+//           divides the tile's stage count where one fits, so every slot
+//           address is compile-time; L2-resident: every tile reads the same
+//           weights);
 //   operands: the next stage's A (weights) and B (image) fragments are read
 //           from LDS while the current stage's MFMAs run (two register sets),
 //           so no wave waits on LDS latency at a stage start;
