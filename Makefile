@@ -42,10 +42,16 @@ build/hip/%.o: dcvc_amd/csrc/hip/%.hip $(HIP_HDRS)
 	@mkdir -p build/hip
 	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall $(HIPFLAGS) -c -o $@ $<
 
-$(LIB)/libdcvc_hip.so: $(HIP_OBJS) scripts/check_isa.sh
+# check_isa.sh: no packed-f32 VALU, no scratch in the split kernels;
+# check_xconv_vmcnt.py: every xconv3_kernel instantiation issues exactly the
+# vector-memory instructions its exact vmcnt waits count (the library is
+# linked to a temporary name first and only kept if the check passes)
+$(LIB)/libdcvc_hip.so: $(HIP_OBJS) scripts/check_isa.sh scripts/check_xconv_vmcnt.py
 	@mkdir -p $(LIB)
 	bash scripts/check_isa.sh $(HIP_OBJS)
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(HIP_OBJS)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@.tmp $(HIP_OBJS)
+	$(PYTHON) scripts/check_xconv_vmcnt.py $@.tmp build/hip/xconv.o || { rm -f $@.tmp; exit 1; }
+	mv $@.tmp $@
 
 oracle/_build/liboracle_rans.so: oracle/rans_oracle.c
 	@mkdir -p oracle/_build

@@ -183,6 +183,19 @@ def max_over_ranks(dist, elapsed, device):
     return t.item()
 
 
+def rank_records(dist, rank, world, frames, own, fallbacks=0):
+    """Every rank's own shard: frames coded, its own timed wall time (before
+    the closing barrier) and rate, so a multi-GPU line shows each shard and the
+    slowest rank's distance from the mean (rank order)."""
+    rec = {"rank": rank, "frames": frames, "elapsed_s": round(own, 4), "fps": round(frames / own, 4),
+           "precision_fallbacks": fallbacks}
+    if dist is None or world == 1:
+        return [rec]
+    allr = [None] * world
+    dist.all_gather_object(allr, rec)
+    return sorted(allr, key=lambda r: r["rank"])
+
+
 def shard_seed(rank):
     """Sequence of rank r: its own synthetic sequence (weak scaling)."""
     return 1 + rank
@@ -370,7 +383,8 @@ def parity_check(cap, inet, pnet, args):
     import tempfile
     from oracle import dc_oracle as O
     from oracle import rans_oracle as R
-    from tests.parity import TIE_EPS, compare_forced, compare_frame
+    from tests.parity import (IDX_TIE_EPS, PSNR_DB, REC_MAXABS, SYM_TIE_EPS, TIE_EPS, compare_forced, compare_frame,
+                              idx_allowed, rec_maxabs)
 
     def psnr(a, x):
         mse = torch.mean((a.float().cpu()[..., :cap["h"], :cap["w"]].clamp(0, 1) - x[..., :cap["h"], :cap["w"]]) ** 2)
@@ -396,11 +410,14 @@ def parity_check(cap, inet, pnet, args):
             enc = [(sy, ix) for k, sy, ix in tr if k == "enc"]
             st = compare_frame(enc, cap["calls"][t], cap["taps"][t])
             ff = st["first_flip"]
+            hw = (slice(None), slice(None), slice(0, cap["h"]), slice(0, cap["w"]))
             row = {"frame": "IP"[t], "symbols": st["symbols"], "sym_diff": st["sym_diff"],
                    "idx_diff": st["idx_diff"], "unexplained": len(st["unexplained"]),
+                   "idx_ties": st["idx_diff_compared"], "idx_ties_allowed": idx_allowed(st["idx_compared"]),
                    "first_flip_tie_dist": max(ff["tie_dist"]) if ff else None,
                    "bits": int(r["bit"]), "bits_oracle": int(cap["bits"][t]),
-                   "dpsnr_db": psnr(rec, xp) - psnr(cap["recon"][t], xp)}
+                   "dpsnr_db": psnr(rec, xp) - psnr(cap["recon"][t], xp),
+                   "rec_maxabs": rec_maxabs(rec[hw].float().cpu().clamp(0, 1), cap["recon"][t][hw].clamp(0, 1))}
             if st["sym_diff"]:
                 # the cascade, element by element: the oracle replays the
                 # product's symbols at its ties (tests/parity.py)
@@ -421,15 +438,26 @@ def parity_check(cap, inet, pnet, args):
                 sf = compare_forced(enc, calls_f, tap, fr.forced)
                 row["replay"] = {"forced": sf["forced"], "sym_diff": sf["sym_diff"], "idx_diff": sf["idx_diff"],
                                  "unexplained": len(sf["unexplained"]), "bits_replay": int(bits_f),
-                                 "dpsnr_db": psnr(rec, xp) - psnr(rec_f, xp)}
+                                 "dpsnr_db": psnr(rec, xp) - psnr(rec_f, xp),
+                                 "rec_maxabs": rec_maxabs(rec[hw].float().cpu().clamp(0, 1), rec_f[hw].clamp(0, 1))}
             out.append(row)
-    ok = all(r["unexplained"] == 0 and ("replay" not in r or (r["replay"]["unexplained"] == 0 and
-                                                                abs(r["replay"]["dpsnr_db"]) < 1e-4)) for r in out)
+
+    def frame_ok(r):
+        if r["unexplained"] or r["idx_ties"] > r["idx_ties_allowed"]:
+            return False
+        if "replay" not in r:
+            return r["sym_diff"] > 0 or (abs(r["dpsnr_db"]) < PSNR_DB and r["rec_maxabs"] <= REC_MAXABS)
+        f = r["replay"]
+        return (f["unexplained"] == 0 and abs(f["dpsnr_db"]) < PSNR_DB
+                and (f["sym_diff"] > 0 or f["rec_maxabs"] <= REC_MAXABS))
+    ok = all(frame_ok(r) for r in out)
     return {"teacher_forced": out, "passed": ok,
-            "bar": f"tests/parity.py: every differing symbol / index a rounding tie (< {TIE_EPS:g} from the "
-                   "discontinuity); after a flipped symbol the oracle replays the product's symbols at its ties and "
-                   "every element of the rest of the frame is checked the same way; identical calls give identical "
-                   "bits and dPSNR < 1e-4 dB (against the replay when a symbol flipped)"}
+            "bar": f"tests/parity.py: every differing symbol a rounding tie (< {SYM_TIE_EPS:g} from the half-integer), "
+                   f"every differing index a tie (< {IDX_TIE_EPS:g} from the integer) and at most "
+                   "max(8, 1e-4 x compared) of them per frame; after a flipped symbol the oracle replays the product's "
+                   "symbols at its ties and every element of the rest of the frame is checked the same way; identical "
+                   f"calls give identical bits, dPSNR < {PSNR_DB:g} dB and decoded pixels within {REC_MAXABS:g} "
+                   "(against the replay when a symbol flipped)"}
 
 
 def launch_ranks(args):
@@ -550,9 +578,11 @@ def launcher_selftest(args):
     plans = [None] * world
     dist.all_gather_object(plans, {"rank": rank, "share": share, "coder_workers": L.dcvc_rans_threads(),
                                    "set_rc": set_rc, "coders": len(coders), "threads": nthreads})
+    ranks = rank_records(dist, rank, world, args.lanes * args.steps, 0.001 * (rank + 1))
     if rank == 0:
         print(json.dumps({"n_gpus": world, "ranks_joined": int(t[0]), "rank_sum": int(t[1]),
-                          "max_elapsed": elapsed, "requested": args.gpus, "plans": plans}), flush=True)
+                          "max_elapsed": elapsed, "requested": args.gpus, "plans": plans, "ranks": ranks}),
+              flush=True)
     dist.destroy_process_group()
 
 
@@ -854,9 +884,15 @@ def main():
     t0 = time.time()
     run_all(timed_idx, True)
     torch.cuda.synchronize(device)
+    own = time.time() - t0
     if dist is not None:
         dist.barrier()
     elapsed = max_over_ranks(dist, time.time() - t0, device)
+    # frames re-coded on the fp32 twin after the split range guard tripped
+    # (layers.split_guarded): such a frame is timed on the fp32 kernels, so
+    # the line counts them, and the metric is flagged when any occurred
+    fallbacks = sum(getattr(net, "fallbacks", 0) for ln in lanes for net in (ln.inet, ln.pnet))
+    ranks = rank_records(dist, rank, world, args.lanes * args.steps, own, fallbacks)
 
     def step(i):   # one more frame on lane 0 (the roofline P-frame below)
         lanes[0].run([i], False)
@@ -987,16 +1023,27 @@ def main():
                        # steady-state GOP mix from the per-frame latencies: lanes x
                        # gop / (t_I + (gop - 1) t_P), every lane count
                        **({"fps_gop_avg": round(args.lanes * args.gop / (float(np.mean(ti))
-                                                                        + (args.gop - 1) * float(np.mean(tp))), 3)}
+                                                                        + (args.gop - 1) * float(np.mean(tp))), 3),
+                           "fps_gop_avg_note": (f"value times {n_i} I-frame(s) in {len(kinds)} frames (1 in "
+                                                f"{len(kinds) / max(n_i, 1):.0f}); the sequence has 1 in {args.gop}: "
+                                                "fps_gop_avg is lanes x gop / (ms_I + (gop - 1) ms_P), the rate at "
+                                                "the sequence's own I-frame share")}
                           if ti and tp else {}),
                        "step": f"one frame on each of {args.lanes} lane(s)",
                        "bpp": round(float(np.mean(timed_bits)) / (h * w), 5), **psnr,
                        **({"bits_per_lane": [int(sum(ln.bits[i] for i in timed_idx)) for ln in lanes]}
                           if args.lanes > 1 else {})},
+            "precision_fallbacks": sum(r["precision_fallbacks"] for r in ranks),
+            **({"ranks": ranks, "rank_fps_spread": {
+                "min": min(r["fps"] for r in ranks), "mean": round(float(np.mean([r["fps"] for r in ranks])), 4),
+                "max": max(r["fps"] for r in ranks)}} if world > 1 else {}),
             "roofline": roof,
             "cpu_baseline": cpu,
             "parity_check": parity,
         }
+        if line["precision_fallbacks"]:
+            line["metric"] += (f" [{line['precision_fallbacks']} frame(s) re-coded on the fp32 twin after the split "
+                               "range guard tripped: not all timed frames ran in split precision]")
         print(json.dumps(line), flush=True)
     import shutil
     shutil.rmtree(out_root, ignore_errors=True)

@@ -553,8 +553,10 @@ extern "C" int dcvc_internal_dconv(const dcvc_conv_args *a, void *stream) {
   p.slope = a->slope;
   p.bias = a->bias;
   p.scale = a->scale;
-  // 32-bit element offsets of the input and output maps
-  if ((int64_t)p.H * p.W * p.xcs >= ((int64_t)1 << 29) || (int64_t)p.Ho * p.Wo * 4 * p.ycs >= ((int64_t)1 << 29))
+  // 32-bit element offsets of the input and output maps; the input's buffer
+  // record is clamped to 0x7fff0000 bytes (kernel), so a larger input map
+  // would read zeros in its last 64 KiB: refused here instead
+  if ((int64_t)p.H * p.W * p.xcs * 4 >= 0x7fff0000 || (int64_t)p.Ho * p.Wo * 4 * p.ycs >= ((int64_t)1 << 29))
     return DCVC_HIP_EUNSUPPORTED;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   // cout < 16: one 16-row block, rows past cout are zero weights, their

@@ -442,7 +442,8 @@ extern "C" int dcvc_depth_conv_split(const dcvc_dc_args *a, void *stream) {
   if (a->x.cstride % 4 || a->x.coff % 4 || a->y.cstride % 4 || a->y.coff % 4 || ((uintptr_t)a->x.ptr & 15) ||
       ((uintptr_t)a->y.ptr & 15))
     return DCVC_HIP_EUNSUPPORTED;
-  if ((int64_t)a->x.H * a->x.W * a->x.cstride * 4 >= ((int64_t)1 << 31) - 64) return DCVC_HIP_EUNSUPPORTED;
+  // (the kernel clamps the input's buffer record to 0x7fff0000 bytes)
+  if ((int64_t)a->x.H * a->x.W * a->x.cstride * 4 >= 0x7fff0000) return DCVC_HIP_EUNSUPPORTED;
   DP p{};
   p.ovf = dcvc_internal_split_flag();
   p.x = reinterpret_cast<const float *>(a->x.ptr);

@@ -433,7 +433,8 @@ extern "C" int dcvc_conv_ffn(const dcvc_ffn_args *a, void *stream) {
   p.b2 = a->b2;
   p.scale = a->scale;
   p.slope = a->slope;
-  if ((int64_t)p.npix * p.xcs * 4 >= ((int64_t)1 << 31) - 64) return DCVC_HIP_EUNSUPPORTED;
+  // (the kernel clamps the input's buffer record to 0x7fff0000 bytes)
+  if ((int64_t)p.npix * p.xcs * 4 >= 0x7fff0000) return DCVC_HIP_EUNSUPPORTED;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   // 8 waves (two per SIMD) of two 16-pixel tiles with every slice resident
   // (C <= 64); C = 128 streams its 16 slices through four 32 KiB buffers, to

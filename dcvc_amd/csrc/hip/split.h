@@ -153,6 +153,33 @@ __device__ __forceinline__ void raw_barrier() {
 }
 __device__ __forceinline__ void wait_lgkm() { __builtin_amdgcn_s_waitcnt(0xC07F); }      // lgkmcnt(0)
 
+// 16-byte LDS read that hipcc's wait insertion does not see.  hipcc puts a
+// vmcnt(0) in front of a plain LDS read of the kernels' constant tables while
+// LDS-DMAs are in flight (it cannot tell that they write elsewhere), so the
+// read would wait for the newest weight DMA of the stage, a memory round trip
+// (xconv's epilogue: DESIGN.md section 9.0).  The caller waits for the reads
+// with lds_wait4 before it uses them.
+__device__ __forceinline__ f32x4 lds_read16(const float *p) {
+  f32x4 r;
+#ifdef __HIP_DEVICE_COMPILE__
+  const uint32_t a = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) float *)p;
+  asm volatile("ds_read_b128 %0, %1" : "=v"(r) : "v"(a));
+#else
+  std::memcpy(&r, p, sizeof r);
+#endif
+  return r;
+}
+// lgkmcnt(0), ordered before every later use of v[0 .. N) (each value passes
+// through an empty volatile asm after the wait)
+template <int N>
+__device__ __forceinline__ void lds_wait4(f32x4 (&v)[N]) {
+#ifdef __HIP_DEVICE_COMPILE__
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int i = 0; i < N; ++i) asm volatile("" : "+v"(v[i]));
+#endif
+}
+
 // host f32 -> f16, round to nearest even (subnormals kept; |v| < 65520 assumed)
 static inline uint16_t host_f2h(float v) {
   uint32_t u;

@@ -42,7 +42,9 @@
 
 #include <algorithm>
 #include <cstring>
+#include <string>
 #include <utility>
+#include <vector>
 
 namespace {
 
@@ -110,6 +112,13 @@ struct XG {
   // the chunk loaded: a last chunk of 8 or 16 channels has fewer pieces), tile
   // loads (res, res2), epilogue stores
   static constexpr int NTILE = NRES * RW * NT;
+  // stages that publish an image piece, and the tile's last stage, issue
+  // their weight DMA after that work (its epilogue stores then precede the
+  // DMA).  hipcc's own vmcnt waits do not count LDS-DMAs, so its wait for a
+  // published piece's loads, and its wait before the epilogue's LDS reads,
+  // also waited for a DMA issued a few instructions earlier: a memory round
+  // trip per tile in each case
+  static constexpr bool DMA_LATE = true;
   static constexpr int NSTORE = RW * NT;
   // image loads of stage x: a chunk's first stage loads the next chunk (of
   // this tile, or the next tile's first).  Exact, not an upper bound: a count
@@ -119,14 +128,29 @@ struct XG {
     if (st_row_(x) != 0) return 0;
     const int c = x < (CH - 1) * KT ? x / KT : CH - 1;
     const int cl = c + 1 < CH ? c + 1 : 0;
+#ifdef XCONV_DEAD_LOAD_PROBE
+    // (tests/test_xconv_vmcnt_check.py: round 5's count, every chunk's load
+    // counted at the larger piece count, which the emitted code contradicts)
+    return 2 * PPM;
+#endif
     return 2 * (cl == CH - 1 ? PPL : PPF);
   }
   // vector-memory instructions per thread issued by stage x of a tile after
   // its weight DMA, and in all
   static constexpr int after_dma(int x) {
-    return img_ops(x) + (x == 0 ? NTILE : 0) + (x == NST - 1 ? NSTORE : 0);
+    return img_ops(x) + (x == 0 ? NTILE : 0) + (x == NST - 1 && !DMA_LATE ? NSTORE : 0);
   }
   static constexpr int all_ops(int x) { return DPW + after_dma(x); }
+  // does stage x publish (a piece of) the next chunk's image (the kernel's step 6)
+  static constexpr bool publishes(int x) {
+    const int c = x < (CH - 1) * KT ? x / KT : CH - 1, rr = st_row_(x);
+    const int rows = c == CH - 1 ? ROWSL : KT;
+    const int cn = c + 1 < CH ? c + 1 : 0;
+    const int ppn = cn == CH - 1 ? PPL : PPF;
+    const int pend = bar(x - rr + rows - 2) ? rows - 2 : rows - 3;
+    const int w0 = pend + 1 - ppn;
+    return w0 >= 1 ? (rr >= w0 && rr <= pend) : rr == pend;
+  }
   static constexpr int st_row_(int x) { return x < (CH - 1) * KT ? x % KT : x - (CH - 1) * KT; }
   // stage s + 1 reads the weight fragments of stage s + 2 (after its MFMAs),
   // so at the end of stage s the weights of stage s + 2 must have landed:
@@ -265,14 +289,38 @@ xconv3_kernel(XP p) {
 
   struct TI {
     int oy0, ox0, n0;
+    int nb, tx, ty;   // n-block, tile column, tile row
   };
   auto tile_of = [&](int t) {
     const int nb = t % p.nblk, sp = t / p.nblk;
     const int ty = sp / p.tiles_x;
     TI r;
+    r.nb = nb;
+    r.ty = ty;
+    r.tx = sp - ty * p.tiles_x;
     r.n0 = nb * BN;
     r.oy0 = ty * G::TH;
-    r.ox0 = (sp - ty * p.tiles_x) * 16;
+    r.ox0 = r.tx * 16;
+    return r;
+  };
+  // tile t + GR from tile t: the grid stride split once into n-block, column
+  // and row steps, so a tile's coordinates cost a few adds instead of
+  // tile_of's four divisions (~100 scalar instructions at every tile start,
+  // issued by every wave of the CU ahead of the tile's first MFMAs)
+  const int dsp = GR / p.nblk, dnb = GR - dsp * p.nblk;
+  const int dty = dsp / p.tiles_x, dtx = dsp - dty * p.tiles_x;
+  auto tile_next = [&](const TI &a) {
+    TI r;
+    r.nb = a.nb + dnb;
+    const int c1 = r.nb >= p.nblk;
+    if (c1) r.nb -= p.nblk;
+    r.tx = a.tx + dtx + c1;
+    const int c2 = r.tx >= p.tiles_x;
+    if (c2) r.tx -= p.tiles_x;
+    r.ty = a.ty + dty + c2;
+    r.n0 = r.nb * BN;
+    r.oy0 = r.ty * G::TH;
+    r.ox0 = r.tx * 16;
     return r;
   };
 
@@ -536,16 +584,24 @@ xconv3_kernel(XP p) {
                                              0x7fff0000, 0x00020000);
     const bool full = full_tile(ti);
     const int px = wave * RW * p.Wo + ti.ox0 + col, n = ti.n0 + hi * 4;
+    // offsets computed unconditionally, then selected: a select whose
+    // offset needs a multiply became a branch with a load on each side,
+    // issuing two counted loads on a wave whose lanes diverge
+    // (scripts/check_xconv_vmcnt.py)
+    const int rows_ok = p.Ho - ti.oy0 - wave * RW;   // wave-uniform
+    const bool lane_ok = ti.ox0 + col < p.Wo;
+    const int o1b = (px * p.rcs + n) * 4, r1row = p.Wo * p.rcs * 4;
+    const int o2b = (px * p.r2cs + n) * 4, r2row = p.Wo * p.r2cs * 4;
 #pragma unroll
     for (int r = 0; r < RW; ++r)
 #pragma unroll
       for (int j = 0; j < NT; ++j) {
-        const bool ok = full || piece_ok(ti, r, j);
-        const int o1 = ok ? ((px + r * p.Wo) * p.rcs + n + j * 16) * 4 : 0x7ffffff0;
+        const bool ok = full | ((r < rows_ok) & lane_ok & (n + j * 16 < p.cout));
+        const int o1 = ok ? o1b + r * r1row + j * 64 : 0x7ffffff0;
         if constexpr (NRES >= 1)
           rv1[r][j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r1, o1, 0, 0));
         if constexpr (NRES >= 2) {
-          const int o2 = ok ? ((px + r * p.Wo) * p.r2cs + n + j * 16) * 4 : 0x7ffffff0;
+          const int o2 = ok ? o2b + r * r2row + j * 64 : 0x7ffffff0;
           rv2[r][j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r2, o2, 0, 0));
         }
       }
@@ -557,17 +613,33 @@ xconv3_kernel(XP p) {
         p.y + (int64_t)ti.oy0 * p.Wo * p.ycs + p.yco, (short)0, 0x7fff0000, 0x00020000);
     const bool full = full_tile(ti);
     const int px = wave * RW * p.Wo + ti.ox0 + col, n = ti.n0 + hi * 4;
+    // bias (and scale) of the lane's channels, read past the compiler's wait
+    // insertion (lds_read16: a plain read here waited for the stage's newest
+    // weight DMA)
+    f32x4 bb[NT];
+#pragma unroll
+    for (int j = 0; j < NT; ++j) bb[j] = lds_read16(Lc + (n + j * 16 < p.cout ? n + j * 16 : 0));
+    constexpr int NSC = SHUF ? (NT % 4 == 0 ? NT / 4 : NT) : NT;
+    f32x4 sc[NSC];
+#pragma unroll
+    for (int k = 0; k < NSC; ++k) {
+      int cb;
+      if constexpr (!SHUF) cb = n + k * 16 < p.cout ? n + k * 16 : 0;
+      else if constexpr (NT % 4 == 0) cb = (ti.n0 >> 2) + 16 * k + 4 * hi;
+      else cb = (ti.n0 >> 2) + 4 * k;
+      sc[k] = lds_read16(Lc + p.cout + cb);
+    }
+    lds_wait4(bb);
+    lds_wait4(sc);
     f32x4 v[RW][NT];
 #pragma unroll
     for (int r = 0; r < RW; ++r)
 #pragma unroll
       for (int j = 0; j < NT; ++j) {
-        const int nc = n + j * 16 < p.cout ? n + j * 16 : 0;
-        const float4 bb = *reinterpret_cast<const float4 *>(Lc + nc);
-        v[r][j][0] = (am[r][j][0] + ac[r][j][0] * kLoInv) + bb.x;
-        v[r][j][1] = (am[r][j][1] + ac[r][j][1] * kLoInv) + bb.y;
-        v[r][j][2] = (am[r][j][2] + ac[r][j][2] * kLoInv) + bb.z;
-        v[r][j][3] = (am[r][j][3] + ac[r][j][3] * kLoInv) + bb.w;
+        v[r][j][0] = (am[r][j][0] + ac[r][j][0] * kLoInv) + bb[j][0];
+        v[r][j][1] = (am[r][j][1] + ac[r][j][1] * kLoInv) + bb[j][1];
+        v[r][j][2] = (am[r][j][2] + ac[r][j][2] * kLoInv) + bb[j][2];
+        v[r][j][3] = (am[r][j][3] + ac[r][j][3] * kLoInv) + bb[j][3];
       }
     if (p.act == DCVC_ACT_LRELU) {
 #pragma unroll
@@ -575,7 +647,7 @@ xconv3_kernel(XP p) {
 #pragma unroll
         for (int j = 0; j < NT; ++j)
 #pragma unroll
-          for (int e = 0; e < 4; ++e) v[r][j][e] = fmaxf(v[r][j][e], v[r][j][e] * p.slope);
+          for (int e = 0; e < 4; ++e) v[r][j][e] = lrelu_in(v[r][j][e], p.slope);
     }
     if constexpr (SHUF) {
       // pixel shuffle (r = 2): conv channel 4 c + 2 dy + dx of pixel (oy, ox)
@@ -586,6 +658,11 @@ xconv3_kernel(XP p) {
       // sub-pixel hi; then the output-channel scale
       const __amdgpu_buffer_rsrc_t ys = __builtin_amdgcn_make_buffer_rsrc(
           p.y + (int64_t)(2 * ti.oy0) * (2 * p.Wo) * p.ycs + p.yco, (short)0, 0x7fff0000, 0x00020000);
+      // store offsets from per-lane bases and uniform steps, selected (no
+      // branch, see load_res): output row 2 (wave RW + r) + dy, column
+      // 2 (ox0 + col) + dx
+      const int srow = 2 * p.Wo * p.ycs * 4, scol = p.ycs * 4;
+      const int sbase = ((2 * wave * RW * 2 * p.Wo + 2 * (ti.ox0 + col)) * p.ycs + (ti.n0 >> 2)) * 4;
 #pragma unroll
       for (int r = 0; r < RW; ++r) {
         uint32_t sh[4][4];   // a group of four j (NT % 4 == 0)
@@ -596,8 +673,7 @@ xconv3_kernel(XP p) {
           uint32_t x0 = __float_as_uint(v[r][j][0]), x1 = __float_as_uint(v[r][j][1]);
           uint32_t x2 = __float_as_uint(v[r][j][2]), x3 = __float_as_uint(v[r][j][3]);
           xpose4(x0, x1, x2, x3);
-          const int ry0 = 2 * (wave * RW + r), cx0 = 2 * (ti.ox0 + col);
-          const bool okp = ti.oy0 + wave * RW + r < p.Ho && ti.ox0 + col < p.Wo;
+          const bool okp = (ti.oy0 + wave * RW + r < p.Ho) & (ti.ox0 + col < p.Wo);
           if constexpr (NT % 4 == 0) {
             // groups of four j: a second transpose, across (row, j), gives
             // row hi the output channels (n0 + 64 g) / 4 + 4 hi .. + 3 of
@@ -611,32 +687,31 @@ xconv3_kernel(XP p) {
             if (k == 3) {
 #pragma unroll
               for (int e = 0; e < 4; ++e) xpose4(sh[0][e], sh[1][e], sh[2][e], sh[3][e]);
-              const int cb = (ti.n0 >> 2) + 16 * g + 4 * hi;
-              const float4 sc = *reinterpret_cast<const float4 *>(Lc + p.cout + cb);
-              const bool ok = okp && ti.n0 + 64 * g + 16 * hi < p.cout;   // (row hi: conv block j = 4 g + hi)
+              const bool ok = okp & (ti.n0 + 64 * g + 16 * hi < p.cout);   // (row hi: conv block j = 4 g + hi)
 #pragma unroll
               for (int s = 0; s < 4; ++s) {
                 f32x4 o;
-                o[0] = __uint_as_float(sh[s][0]) * sc.x;
-                o[1] = __uint_as_float(sh[s][1]) * sc.y;
-                o[2] = __uint_as_float(sh[s][2]) * sc.z;
-                o[3] = __uint_as_float(sh[s][3]) * sc.w;
-                const int ry = ry0 + (s >> 1), cx = cx0 + (s & 1);
-                const int off = ok ? ((ry * 2 * p.Wo + cx) * p.ycs + cb) * 4 : 0x7ffffff0;
+                o[0] = __uint_as_float(sh[s][0]) * sc[g][0];
+                o[1] = __uint_as_float(sh[s][1]) * sc[g][1];
+                o[2] = __uint_as_float(sh[s][2]) * sc[g][2];
+                o[3] = __uint_as_float(sh[s][3]) * sc[g][3];
+                // pixel (ry0 + (s >> 1), cx0 + (s & 1)), channels (n0 >> 2) + 16 g + 4 hi ..
+                int off = ok ? sbase + (2 * r + (s >> 1)) * srow + (s & 1) * scol + (16 * g + 4 * hi) * 4
+                             : 0x7ffffff0;
+                opaque_v(off);   // (one store: hipcc otherwise duplicated it into both sides of a branch)
                 __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, o), ys, off, 0, 0);
               }
             }
           } else {
-            const int cb = (ti.n0 >> 2) + 4 * j;
-            const float4 sc = *reinterpret_cast<const float4 *>(Lc + p.cout + cb);
             f32x4 o;
-            o[0] = __uint_as_float(x0) * sc.x;
-            o[1] = __uint_as_float(x1) * sc.y;
-            o[2] = __uint_as_float(x2) * sc.z;
-            o[3] = __uint_as_float(x3) * sc.w;
-            const int ry = ry0 + (hi >> 1), cx = cx0 + (hi & 1);
-            const bool ok = okp && ti.n0 + 16 * j < p.cout;
-            const int off = ok ? ((ry * 2 * p.Wo + cx) * p.ycs + cb) * 4 : 0x7ffffff0;
+            o[0] = __uint_as_float(x0) * sc[j][0];
+            o[1] = __uint_as_float(x1) * sc[j][1];
+            o[2] = __uint_as_float(x2) * sc[j][2];
+            o[3] = __uint_as_float(x3) * sc[j][3];
+            // pixel (ry0 + (hi >> 1), cx0 + (hi & 1)), channels (n0 >> 2) + 4 j ..
+            const bool ok = okp & (ti.n0 + 16 * j < p.cout);
+            int off = ok ? sbase + (2 * r + (hi >> 1)) * srow + (hi & 1) * scol + 16 * j : 0x7ffffff0;
+            opaque_v(off);
             __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, o), ys, off, 0, 0);
           }
         }
@@ -664,20 +739,23 @@ xconv3_kernel(XP p) {
       for (int r = 0; r < RW; ++r)
 #pragma unroll
         for (int j = 0; j < NT; ++j) {
-          const int nc = n + j * 16 < p.cout ? n + j * 16 : 0;
-          const float4 sc = *reinterpret_cast<const float4 *>(Lc + p.cout + nc);
-          v[r][j][0] *= sc.x;
-          v[r][j][1] *= sc.y;
-          v[r][j][2] *= sc.z;
-          v[r][j][3] *= sc.w;
+          v[r][j][0] *= sc[j][0];
+          v[r][j][1] *= sc[j][1];
+          v[r][j][2] *= sc[j][2];
+          v[r][j][3] *= sc[j][3];
         }
     }
+    // store offsets computed unconditionally, then selected (an offset past
+    // the buffer for pieces outside the output): no per-piece branches
+    const int rows_ok = p.Ho - ti.oy0 - wave * RW;                 // wave-uniform
+    const bool lane_ok = ti.ox0 + col < p.Wo;
+    const int o0 = (px * p.ycs + n) * 4, orow = p.Wo * p.ycs * 4;
 #pragma unroll
     for (int r = 0; r < RW; ++r)
 #pragma unroll
       for (int j = 0; j < NT; ++j) {
-        const bool ok = full || piece_ok(ti, r, j);
-        const int o = ok ? ((px + r * p.Wo) * p.ycs + n + j * 16) * 4 : 0x7ffffff0;
+        const bool ok = full | ((r < rows_ok) & lane_ok & (n + j * 16 < p.cout));
+        const int o = ok ? o0 + r * orow + j * 64 : 0x7ffffff0;
         if (!(XDBG & 128)) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, v[r][j]), yr, o, 0, 0);
       }
   };
@@ -706,9 +784,10 @@ xconv3_kernel(XP p) {
 #endif
   int kw = 0;   // weight slot of the current stage (stage counter mod NSW)
   int q = 0;    // image buffer of the current chunk (chunk counter mod 2)
+  TI tcur = tile_of(g);
   for (int t = g; t < p.ntiles; t += G0) {
-    const int tn = t + G0 < p.ntiles ? t + G0 : t;   // the next tile (prefetch target; itself when last)
-    TI tc = tile_of(t), tx = tile_of(tn);
+    // this tile and the next (prefetch target; itself when last)
+    TI tc = tcur, tx = t + G0 < p.ntiles ? tile_next(tcur) : tcur;
     // computed once per tile: opaque, so the compiler keeps (or spills) them
     // instead of redoing tile_of's divisions in every stage that reads them
     opaque_s(tc.n0), opaque_s(tc.oy0), opaque_s(tc.ox0);
@@ -775,8 +854,11 @@ xconv3_kernel(XP p) {
         }
         if constexpr (s == 0) load_res(tc);
       };
+      // stages that publish an image piece or run the epilogue issue their
+      // weight DMA after that work (G::DMA_LATE)
+      constexpr bool dlate = G::DMA_LATE && (s == NST - 1 || G::publishes(s));
       constexpr bool SPLITMF = DBA && !late;
-      if constexpr (!SPLITMF) issue_mem();
+      if constexpr (!SPLITMF && !dlate) issue_mem();
       // 4. operands of stage s + 1 into the other register set (the next
       // stage's weights landed and were published one barrier ago)
       const int ws1 = kw_ + 1 >= NSW ? 0 : kw_ + 1;
@@ -811,7 +893,7 @@ xconv3_kernel(XP p) {
         });
 #endif
         sched_fence();
-        issue_mem();
+        if constexpr (!dlate) issue_mem();
         sched_fence();
         if (!(XDBG & 1)) mfmas(std::integral_constant<int, S>{}, ws1, std::integral_constant<int, 2>{});
       }
@@ -842,6 +924,10 @@ xconv3_kernel(XP p) {
       }
       // 7. epilogue
       if constexpr (s == NST - 1) epilogue(tc);
+      if constexpr (dlate) {
+        sched_fence();
+        issue_mem();
+      }
       // end of stage: stage s + 2's weights must have landed, every
       // vector-memory operation issued after their DMA may stay in flight
       // (fenced: the scheduler would hoist the wait above the MFMAs, right
@@ -871,12 +957,57 @@ xconv3_kernel(XP p) {
       if constexpr (rr == rows - 1) q ^= 1;
       kw = kw + 1 >= NSW ? 0 : kw + 1;
     });
+    tcur = tx;
   }
   wait_vm_lgkm();   // no LDS-DMA left in flight when the workgroup exits
 #ifdef XCONV_DBG
   if (blockIdx.x == 0 && wave < 8) g_xstamps[wave * 64 + lane] = stampv;
 #endif
 }
+
+// The vector-memory schedule the kernel's exact vmcnt waits assume, per
+// stage: its vector-memory instructions in issue order (D weight LDS-DMA,
+// I image load, R residual load, S output store) and, at a barrier stage,
+// the wait's count.  scripts/check_xconv_vmcnt.py compares it with the
+// instructions hipcc emitted for every instantiation (make runs it): a load
+// the compiler deleted, merged or moved ahead of a DMA, or a spill's scratch
+// access, would make a wait pass with its DMA in flight (the round-5 ring
+// race).  Line per stage: "<ops> <wait or -1>".
+template <int CIN, int BN, int RW, int NW, int NRES, int KS>
+int sched_dump(char *buf, int cap) {
+  typedef XG<CIN, BN, RW, NW, NRES, KS> G;
+  std::string out = "nst " + std::to_string(G::NST) + " nsw " + std::to_string(G::NSW) + "\n";
+  for (int x = 0; x < G::NST; ++x) {
+    const bool dlate = G::DMA_LATE && (x == G::NST - 1 || G::publishes(x));
+    std::string ops;
+    if (!dlate) ops.append(G::DPW, 'D');
+    ops.append(G::img_ops(x), 'I');
+    if (x == 0) ops.append(G::NTILE, 'R');
+    if (x == G::NST - 1) ops.append(G::NSTORE, 'S');
+    if (dlate) ops.append(G::DPW, 'D');
+    out += (ops.empty() ? "-" : ops) + " " + std::to_string(G::bar(x) ? G::wait_n(x) : -1) + "\n";
+  }
+  if ((int)out.size() + 1 > cap) return DCVC_HIP_EINVAL;
+  std::memcpy(buf, out.c_str(), out.size() + 1);
+  return DCVC_HIP_OK;
+}
+
+// every instantiation launch<> uses registers its sched_dump at load time
+struct SchedEntry {
+  int cin, bn, rw, nw, nres, ks;
+  int (*dump)(char *, int);
+};
+std::vector<SchedEntry> &sched_registry() {
+  static std::vector<SchedEntry> r;
+  return r;
+}
+template <int CIN, int BN, int RW, int NW, int NRES, int KS>
+struct SchedReg {
+  SchedReg() { sched_registry().push_back({CIN, BN, RW, NW, NRES, KS, &sched_dump<CIN, BN, RW, NW, NRES, KS>}); }
+  static SchedReg inst;
+};
+template <int CIN, int BN, int RW, int NW, int NRES, int KS>
+SchedReg<CIN, BN, RW, NW, NRES, KS> SchedReg<CIN, BN, RW, NW, NRES, KS>::inst;
 
 int g_cus = 0;
 int g_enable = 1;   // dcvc_set_option("xconv", 0): route every split conv to sconv.hip
@@ -891,6 +1022,7 @@ int g_rw1 = 1;
 template <int CIN, int BN, int RW, int NW, int NRES, bool SHUF = false, int KS = 3>
 int launch(XP p, hipStream_t st) {
   typedef XG<CIN, BN, RW, NW, NRES, KS> G;
+  (void)&SchedReg<CIN, BN, RW, NW, NRES, KS>::inst;   // (scripts/check_xconv_vmcnt.py)
   const size_t lds = G::lds(p.cout);
   if (lds > (size_t)G::LDS_WG) return DCVC_HIP_EUNSUPPORTED;
   p.tiles_x = (p.Wo + 15) / 16;
@@ -962,6 +1094,19 @@ int pick_bn(XP p, hipStream_t st) {
 }
 
 }  // namespace
+
+// scripts/check_xconv_vmcnt.py: the schedule of xconv3_kernel<cin, bn, rw, nw,
+// nres, *, ks> (above), host-side, no GPU needed
+// (index i of the registered instantiations: its parameters into p[6] and its
+// schedule into buf; DCVC_HIP_EINVAL past the last)
+extern "C" int dcvc_internal_xconv_schedule(int i, int *prm, char *buf, int cap) {
+  const auto &r = sched_registry();
+  if (i < 0 || i >= (int)r.size()) return DCVC_HIP_EINVAL;
+  const SchedEntry &e = r[i];
+  const int v[6] = {e.cin, e.bn, e.rw, e.nw, e.nres, e.ks};
+  std::memcpy(prm, v, sizeof v);
+  return e.dump(buf, cap);
+}
 
 extern "C" void dcvc_internal_xconv_enable(int v) { g_enable = v; }
 
@@ -1054,7 +1199,8 @@ extern "C" int dcvc_internal_xconv(const dcvc_conv_args *a, void *stream) {
   if ((int64_t)16 * p.Wo * std::max(p.ycs, std::max(p.rcs, p.r2cs)) * 4 >= ((int64_t)1 << 30))
     return DCVC_HIP_EUNSUPPORTED;
   if (a->shuffle && (int64_t)32 * 2 * p.Wo * p.ycs * 4 >= ((int64_t)1 << 31) - 64) return DCVC_HIP_EUNSUPPORTED;
-  if ((int64_t)(16 + a->kh) * p.W * p.xcs * 4 >= ((int64_t)1 << 31) - 64) return DCVC_HIP_EUNSUPPORTED;
+  // (the halo rows a tile reads fit the input record, clamped to 0x7fff0000 bytes)
+  if ((int64_t)(16 + a->kh) * p.W * p.xcs * 4 >= 0x7fff0000) return DCVC_HIP_EUNSUPPORTED;
   const int nch = (a->cin + 31) / 32;
   const int vc = a->cin - 32 * (nch - 1);
   const int tpkl = vc <= 8 ? 4 : vc <= 16 ? 2 : 1;

@@ -1,0 +1,216 @@
+"""Build-time check of xconv3_kernel's exact vmcnt waits (make runs it).
+
+xconv.hip waits for a stage's weight LDS-DMA with vmcnt(N), N = the count of
+vector-memory instructions issued after that DMA, computed at compile time
+from the schedule the kernel template assumes (XG::after_dma / wait_for).
+That is only right if hipcc emits exactly those instructions in that order.
+Round 5's ring race came from a load the template counted and hipcc deleted
+as dead: the waits then passed with the DMA still in flight (DESIGN.md
+section 9.0).  This script compares, for every instantiation in the built
+library, the template's schedule (dcvc_internal_xconv_schedule, host-side:
+no GPU) with the instructions in the code object:
+
+  * the vector-memory instructions between consecutive stage barriers of the
+    tile loop, in program order, must be exactly the template's (D weight
+    LDS-DMA, L image / residual load, S output store): a deleted, merged,
+    added (a spill's scratch access) or reordered one fails;
+  * the vmcnt of the wait in front of each stage barrier must be the
+    template's (a smaller one is stricter, reported, not fatal).
+
+    python scripts/check_xconv_vmcnt.py dcvc_amd/lib/libdcvc_hip.so build/hip/xconv.o
+    python scripts/check_xconv_vmcnt.py LIB disasm.s      (an llvm-objdump -d listing)
+"""
+import ctypes
+import os
+import re
+import subprocess
+import sys
+import tempfile
+
+LLVM = "/opt/rocm/lib/llvm/bin"
+MANGLED = re.compile(r"xconv3_kernelILi(\d+)ELi(\d+)ELi(\d+)ELi(\d+)ELi(\d+)ELb(\d)ELi(\d+)E")
+
+
+def schedules(lib_path):
+    """{(cin, bn, rw, nw, nres, ks): [(ops, wait)] per stage} of every
+    instantiation the library registered."""
+    lib = ctypes.CDLL(os.path.abspath(lib_path))
+    f = lib.dcvc_internal_xconv_schedule
+    f.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_int), ctypes.c_char_p, ctypes.c_int]
+    f.restype = ctypes.c_int
+    out = {}
+    i = 0
+    while True:
+        prm = (ctypes.c_int * 6)()
+        buf = ctypes.create_string_buffer(1 << 16)
+        if f(i, prm, buf, len(buf)) != 0:
+            break
+        lines = buf.value.decode().strip().split("\n")
+        stages = []
+        for ln in lines[1:]:
+            ops, w = ln.split()
+            stages.append(("" if ops == "-" else ops, int(w)))
+        out[tuple(prm)] = stages
+        i += 1
+    return out
+
+
+def disassemble(obj):
+    """llvm-objdump -d listing of the gfx950 code object inside a host object
+    (its .hip_fatbin), or the listing itself for a .s path."""
+    if obj.endswith(".s"):
+        return open(obj).read()
+    with tempfile.TemporaryDirectory() as td:
+        fat, co = os.path.join(td, "x.fat"), os.path.join(td, "x.co")
+        subprocess.run([f"{LLVM}/llvm-objcopy", f"--dump-section=.hip_fatbin={fat}", obj], check=True)
+        subprocess.run([f"{LLVM}/clang-offload-bundler", "--unbundle", "--type=o",
+                        "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--input={fat}", f"--output={co}"],
+                       check=True)
+        return subprocess.run([f"{LLVM}/llvm-objdump", "-d", co], check=True, capture_output=True,
+                              text=True).stdout
+
+
+def kernels(listing):
+    """{mangled name: [(address, mnemonic, operands, branch target or None)]}
+    of the xconv3_kernel functions."""
+    out, cur, base = {}, None, 0
+    for ln in listing.splitlines():
+        m = re.match(r"^([0-9a-f]+) <(.*)>:", ln)
+        if m:
+            cur = m.group(2) if "xconv3_kernel" in m.group(2) else None
+            base = int(m.group(1), 16)
+            if cur:
+                out[cur] = []
+            continue
+        if cur is None:
+            continue
+        m = re.match(r"\s+([a-z_0-9]+)\s*(.*?)\s*//\s*([0-9A-Fa-f]+):(.*)$", ln)
+        if not m:
+            continue
+        mn, ops, addr, rest = m.group(1), m.group(2), int(m.group(3), 16), m.group(4)
+        t = re.search(r"<[^>+]*\+0x([0-9a-f]+)>", rest)
+        tgt = base + int(t.group(1), 16) if t and mn.startswith("s_") and "branch" in mn else None
+        out[cur].append((addr, mn, ops, tgt))
+    return out
+
+
+def kind(mn, ops):
+    if mn.startswith("scratch_") or mn.startswith("buffer_wbl2") or mn.startswith("buffer_inv"):
+        return "X"
+    if mn.startswith("buffer_load") or mn.startswith("global_load"):
+        return "D" if re.search(r"\blds\b", ops) else "L"
+    if mn.startswith("buffer_store") or mn.startswith("global_store"):
+        return "S"
+    if mn.startswith("buffer_") or mn.startswith("global_") or mn.startswith("flat_"):
+        return "X"
+    return None
+
+
+def vmcnt_of(ops):
+    m = re.search(r"vmcnt\((\d+)\)", ops)
+    return int(m.group(1)) if m else None
+
+
+def check_kernel(name, ins, sched):
+    """Errors and notes for one instantiation.
+
+    The tile loop is the address range from the target of its back-edges to
+    the last of them (hipcc may rotate it, so that its last stage barrier
+    sits at the top).  Its barriers cut it into as many intervals, taken
+    cyclically (the interval that contains the loop's entry runs from the last
+    barrier around to the first); the template's intervals end at its barrier
+    stages, so the two lists must agree under one rotation."""
+    errs, notes = [], []
+    bar_stages = [s for s, (_, w) in enumerate(sched) if w >= 0]
+    nb = len(bar_stages)
+    back = [(a, t) for a, mn, _, t in ins if t is not None and t < a]
+    if not back:
+        return [f"{name}: no loop back-edge"], notes
+    # (the last back-edge is the tile loop's; small loops before it, such as
+    # the prologue's bias copy, lie outside its range)
+    end, top = max(back)
+    body = [(a, mn, ops) for a, mn, ops, _ in ins if top <= a <= end]
+    outside = "".join(c for c in (kind(mn, ops) for a, mn, ops, _ in ins if a > end) if c and c != "S")
+    bars = [i for i, (_, mn, _) in enumerate(body) if mn == "s_barrier"]
+    if len(bars) != nb:
+        return [f"{name}: {len(bars)} barriers in the tile loop, the schedule has {nb} stage barriers"], notes
+    if outside:
+        errs.append(f"{name}: vector-memory instructions {outside} after the tile loop")
+    # the loop's intervals, cyclic: cyc[i] ends at body barrier i
+    cyc = []
+    for i in range(nb):
+        seg = body[bars[i - 1] + 1:bars[i]] if i else body[bars[-1] + 1:] + body[:bars[0]]
+        ops = "".join(c for c in (kind(mn, o) for _, mn, o in seg) if c)
+        w = None
+        for _, mn, o in reversed(seg):
+            if mn == "s_waitcnt" and vmcnt_of(o) is not None:
+                w = vmcnt_of(o)
+                break
+            if kind(mn, o):
+                break
+        cyc.append((ops, w))
+    want = []
+    for k, s in enumerate(bar_stages):
+        prev = bar_stages[k - 1] if k else bar_stages[-1] - len(sched)
+        ops = "".join(sched[x % len(sched)][0] for x in range(prev + 1, s + 1))
+        want.append((ops.replace("I", "L").replace("R", "L"), sched[s][1], f"{prev + 1 if k else 0}..{s}"))
+    best = None
+    for r in range(nb):
+        bad, nts = [], []
+        for i in range(nb):
+            ops, w = cyc[i]
+            wops, ww, rng = want[(i + r) % nb]
+            if ops != wops:
+                bad.append(f"stages {rng}: vector-memory instructions {ops or '-'}, the vmcnt schedule assumes "
+                           f"{wops or '-'}")
+            if w is None:
+                bad.append(f"stages {rng}: no vmcnt wait before the barrier (the schedule's: vmcnt({ww}))")
+            elif w > ww:
+                bad.append(f"stages {rng}: vmcnt({w}) before the barrier, the schedule needs vmcnt({ww})")
+            elif w < ww:
+                nts.append(f"stages {rng}: vmcnt({w}), stricter than the schedule's vmcnt({ww})")
+        if best is None or len(bad) < len(best[0]):
+            best = (bad, nts)
+        if not bad:
+            break
+    errs += [f"{name}: {b}" for b in best[0]]
+    notes += [f"{name}: {n}" for n in best[1]]
+    return errs, notes
+
+
+def main(argv):
+    if len(argv) != 3:
+        print(__doc__)
+        return 2
+    sched = schedules(argv[1])
+    ks = kernels(disassemble(argv[2]))
+    if not ks:
+        print("check_xconv_vmcnt: no xconv3_kernel in", argv[2], file=sys.stderr)
+        return 1
+    errs, notes, seen = [], [], 0
+    for name, ins in sorted(ks.items()):
+        m = MANGLED.search(name)
+        if not m:
+            errs.append(f"{name}: cannot read the template parameters")
+            continue
+        cin, bn, rw, nw, nres, _shuf, k = (int(v) for v in m.groups())
+        key = (cin, bn, rw, nw, nres, k)
+        if key not in sched:
+            errs.append(f"{name}: no schedule registered for {key}")
+            continue
+        e, n = check_kernel(f"xconv3_kernel<{cin},{bn},{rw},{nw},{nres},{_shuf},{k}>", ins, sched[key])
+        errs += e
+        notes += n
+        seen += 1
+    for n in notes:
+        print("check_xconv_vmcnt: note:", n)
+    for e in errs:
+        print("check_xconv_vmcnt:", e, file=sys.stderr)
+    if errs:
+        return 1
+    print(f"check_xconv_vmcnt: {seen} xconv3_kernel instantiations match their vmcnt schedules")
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main(sys.argv))

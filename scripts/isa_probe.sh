@@ -10,7 +10,7 @@ nres=${3:-0}
 rw=${4:-2}
 ks=${5:-3}
 B=/opt/rocm/lib/llvm/bin
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -fno-slp-vectorize -DXCONV_ISA_PROBE=$c -DXCONV_PROBE_BN=$bn -DXCONV_PROBE_NRES=$nres -DXCONV_PROBE_RW=$rw -DXCONV_PROBE_KS=$ks \
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -fno-slp-vectorize -DXCONV_ISA_PROBE=$c -DXCONV_PROBE_BN=$bn -DXCONV_PROBE_NRES=$nres -DXCONV_PROBE_RW=$rw -DXCONV_PROBE_KS=$ks ${XFLAGS:-} \
   --cuda-device-only -c -o /tmp/xprobe$c.co dcvc_amd/csrc/hip/xconv.hip -Rpass-analysis=kernel-resource-usage 2>&1 |
   grep -E "Function Name|VGPRs|AGPRs|Spill" | sed 's/.*remark: *//;s/ \[-Rpass.*//' | paste - - - - - |
   sed 's/_ZN12_GLOBAL__N_113xconv3_kernelI//;s/EEvNS_2XPE//;s/Function Name: //'

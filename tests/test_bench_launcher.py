@@ -31,6 +31,10 @@ def test_bench_gpus_n_launches_n_ranks(n):
     assert len(lines) == 1, r.stdout
     d = json.loads(lines[0])
     assert d["n_gpus"] == n and d["ranks_joined"] == n and d["rank_sum"] == n * (n - 1) // 2 and d["requested"] == n
+    # one shard record per rank, in rank order (the N > 1 bench line's "ranks")
+    assert [r["rank"] for r in d["ranks"]] == list(range(n)), d["ranks"]
+    for r in d["ranks"]:
+        assert r["frames"] > 0 and r["elapsed_s"] > 0 and r["fps"] > 0 and r["precision_fallbacks"] == 0, r
     shares = [set(p["share"]) for p in d["plans"]]
     ncpu = len(os.sched_getaffinity(0))
     if ncpu >= n:
