@@ -51,6 +51,7 @@ $(LIB)/libdcvc_hip.so: $(HIP_OBJS) scripts/check_isa.sh scripts/check_xconv_vmcn
 	bash scripts/check_isa.sh $(HIP_OBJS)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@.tmp $(HIP_OBJS)
 	$(PYTHON) scripts/check_xconv_vmcnt.py $@.tmp build/hip/xconv.o || { rm -f $@.tmp; exit 1; }
+	$(PYTHON) scripts/check_xconv_vmcnt.py $@.tmp build/hip/wconv.o || { rm -f $@.tmp; exit 1; }
 	mv $@.tmp $@
 
 oracle/_build/liboracle_rans.so: oracle/rans_oracle.c

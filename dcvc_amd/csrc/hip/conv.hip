@@ -589,6 +589,8 @@ extern "C" void dcvc_internal_sgemm_gate(int v);
 extern "C" int dcvc_internal_set_option_split(const char *name, int value);
 extern "C" int dcvc_internal_xconv(const dcvc_conv_args *a, void *stream);
 extern "C" void dcvc_internal_xconv_enable(int v);
+extern "C" int dcvc_internal_wconv(const dcvc_conv_args *a, void *stream);
+extern "C" void dcvc_internal_wconv_enable(int v);
 extern "C" int dcvc_internal_dconv(const dcvc_conv_args *a, void *stream);
 extern "C" int dcvc_internal_tconv(const dcvc_conv_args *a, void *stream);
 extern "C" void dcvc_internal_tconv_enable(int v);
@@ -669,6 +671,8 @@ extern "C" int dcvc_conv2d(const dcvc_conv_args *a, void *stream) {
     int r = dcvc_internal_tconv(a, stream);   // 2-channel inputs: fp32 VALU (tconv.hip)
     if (r != DCVC_HIP_EUNSUPPORTED) return r;
     r = dcvc_internal_nconv(a, stream);       // 2- / 3-channel outputs: pixels on M (nconv.hip)
+    if (r != DCVC_HIP_EUNSUPPORTED) return r;
+    r = dcvc_internal_wconv(a, stream);       // wave-specialised 3x3 stride-1 kernel (wconv.hip)
     if (r != DCVC_HIP_EUNSUPPORTED) return r;
     r = dcvc_internal_xconv(a, stream);       // static-shape 3x3 stride-1 kernel (xconv.hip)
     if (r != DCVC_HIP_EUNSUPPORTED) return r;
@@ -829,6 +833,10 @@ extern "C" int dcvc_set_option(const char *name, int value) {
   }
   if (std::strcmp(name, "xconv") == 0) {
     dcvc_internal_xconv_enable(value);
+    return DCVC_HIP_OK;
+  }
+  if (std::strcmp(name, "wconv") == 0) {
+    dcvc_internal_wconv_enable(value);
     return DCVC_HIP_OK;
   }
   if (std::strcmp(name, "dconv") == 0) {

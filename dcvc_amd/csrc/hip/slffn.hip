@@ -39,8 +39,21 @@
 namespace {
 
 constexpr int kNW = 4, kNT = kNW * 64;
-constexpr int P = 32;     // pixels per workgroup (two 16-pixel MFMA column blocks)
+
 constexpr int HS = 64;    // hidden channels per slice (4 row blocks: one per wave)
+// pixel blocks (16 pixels each) per workgroup of slffn_kernel<384>.  Every
+// workgroup streams the block's whole packed weight set (3.1 MB of hi / lo
+// fragments at C = 384) from L2 into registers; 4 blocks halve those L2
+// bytes per pixel and the grid, but measured 100 vs 60 us (sldc 59 vs 34 us,
+// profiles/r06c_latent_pb_ab.jsonl): the time follows the MFMAs of its one
+// wave per SIMD, not the L2 bytes, so 2 stays.
+#ifndef SLFFN_PB384
+#define SLFFN_PB384 2
+#endif
+// the same for sldc_kernel<384> (the conv2 weights: 0.6 MB per workgroup)
+#ifndef SLDC_PB384
+#define SLDC_PB384 2
+#endif
 constexpr int kOob = 0x7fffffe0;
 
 struct LP {
@@ -60,9 +73,10 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void *base, int byt
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), (short)0, bytes, 0x00020000);
 }
 
-template <int C>
+template <int C, int PB>
 __global__ void __launch_bounds__(kNT) slffn_kernel(LP p) {
   SplitRange rg(p.ovf);
+  constexpr int P = 16 * PB;        // pixels per workgroup
   constexpr int KC = C / 32;        // ffn1 K chunks
   constexpr int NTW = C / 64;       // ffn2 output row blocks per wave
   constexpr int XI = KC * P * 32;   // halves of the input image (hi or lo)
@@ -123,11 +137,11 @@ __global__ void __launch_bounds__(kNT) slffn_kernel(LP p) {
   }
   __syncthreads();
 
-  f32x4 om[NTW][2], oc[NTW][2];
+  f32x4 om[NTW][PB], oc[NTW][PB];
 #pragma unroll
   for (int j = 0; j < NTW; ++j)
 #pragma unroll
-    for (int pb = 0; pb < 2; ++pb) {
+    for (int pb = 0; pb < PB; ++pb) {
       om[j][pb] = f32x4{0.f, 0.f, 0.f, 0.f};
       oc[j][pb] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
@@ -142,16 +156,16 @@ __global__ void __launch_bounds__(kNT) slffn_kernel(LP p) {
       for (int kk = 0; kk < 2; ++kk) ldfrag(w2r, (wave * NTW + j) * KH + 2 * s + kk, a2h[j][kk], a2l[j][kk]);
 
     // ffn1: hidden rows s * 64 + 16 wave .. + 15 for both pixel blocks
-    f32x4 hm[2], hc[2];
+    f32x4 hm[PB], hc[PB];
 #pragma unroll
-    for (int pb = 0; pb < 2; ++pb) {
+    for (int pb = 0; pb < PB; ++pb) {
       hm[pb] = f32x4{0.f, 0.f, 0.f, 0.f};
       hc[pb] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
 #pragma unroll
     for (int kc = 0; kc < KC; ++kc)
 #pragma unroll
-      for (int pb = 0; pb < 2; ++pb) {
+      for (int pb = 0; pb < PB; ++pb) {
         const int o = swz(kc * P + pb * 16 + col, g);
         const f16x8 bh = *reinterpret_cast<const f16x8 *>(Xh + o);
         const f16x8 bl = *reinterpret_cast<const f16x8 *>(Xl + o);
@@ -170,7 +184,7 @@ __global__ void __launch_bounds__(kNT) slffn_kernel(LP p) {
     // (g & 1) * 4 .. + 3 of the slot
     uint16_t *Hh = Hb + (s & 1) * 2 * HI, *Hl = Hh + HI;
 #pragma unroll
-    for (int pb = 0; pb < 2; ++pb) {
+    for (int pb = 0; pb < PB; ++pb) {
       float v[4];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
@@ -191,11 +205,13 @@ __global__ void __launch_bounds__(kNT) slffn_kernel(LP p) {
     // every wave's hidden rows of slice s are in; (every wave finished ffn2
     // of slice s - 1 before it got here, so buffer (s + 1) & 1 is free next)
     __syncthreads();
-    // ffn2 over the slice: K chunks 2 s, 2 s + 1 of the hidden layer
+    // ffn2 over the slice: K chunks 2 s, 2 s + 1 of the hidden layer (the
+    // image operands read at their use: a register ring here and in ffn1
+    // measured 26.8 vs 24.8 us at C = 192, profiles/r06f_lat_ab.jsonl)
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
-      for (int pb = 0; pb < 2; ++pb) {
+      for (int pb = 0; pb < PB; ++pb) {
         const int o = swz(kk * P + pb * 16 + col, g);
         const f16x8 bh = *reinterpret_cast<const f16x8 *>(Hh + o);
         const f16x8 bl = *reinterpret_cast<const f16x8 *>(Hl + o);
@@ -212,7 +228,7 @@ __global__ void __launch_bounds__(kNT) slffn_kernel(LP p) {
   // (wave * NTW + j) * 16 + 4 g .. + 3 of pixel pix0 + pb * 16 + col
   const __amdgpu_buffer_rsrc_t yr = rsrc(p.y + p.yco, p.ybytes);
 #pragma unroll
-  for (int pb = 0; pb < 2; ++pb) {
+  for (int pb = 0; pb < PB; ++pb) {
     const int px = pix0 + pb * 16 + col;
     const bool ok = px < p.npix;
     f32x4 xv[NTW];
@@ -265,9 +281,10 @@ struct DP {
   int *ovf;               // fp16 range guard (split.h SplitRange)
 };
 
-template <int C>
+template <int C, int PB>
 __global__ void __launch_bounds__(kNT) sldc_kernel(DP p) {
   SplitRange rg(p.ovf);
+  constexpr int P = 16 * PB;        // pixels per workgroup
   constexpr int KC = C / 32, NTW = C / 64, PF = 2;
   constexpr int XI = KC * P * 32;
   extern __shared__ __align__(16) unsigned char smem[];
@@ -343,28 +360,39 @@ __global__ void __launch_bounds__(kNT) sldc_kernel(DP p) {
   }
   __syncthreads();
 
-  f32x4 am[NTW][2], ac[NTW][2];
+  f32x4 am[NTW][PB], ac[NTW][PB];
 #pragma unroll
   for (int j = 0; j < NTW; ++j)
 #pragma unroll
-    for (int pb = 0; pb < 2; ++pb) {
+    for (int pb = 0; pb < PB; ++pb) {
       am[j][pb] = f32x4{0.f, 0.f, 0.f, 0.f};
       ac[j][pb] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
+  // (the image operands one K chunk ahead in a second register set: 12.4 vs
+  // 13.5 us at C = 192, 34.2 vs 34.5 at 384, profiles/r06f_lat_ab.jsonl)
+  f16x8 rbh[2][PB], rbl[2][PB];
+  auto rd2 = [&](int kc, int q) {
+#pragma unroll
+    for (int pb = 0; pb < PB; ++pb) {
+      const int o = swz(kc * P + pb * 16 + col, g);
+      rbh[q][pb] = *reinterpret_cast<const f16x8 *>(Dh + o);
+      rbl[q][pb] = *reinterpret_cast<const f16x8 *>(Dl + o);
+    }
+  };
+  rd2(0, 0);
 #pragma unroll
   for (int kc = 0; kc < KC; ++kc) {
     if (kc + PF < KC) ldw(kc + PF, (kc + PF) % (PF + 1));
-    const int q = kc % (PF + 1);
+    if (kc + 1 < KC) rd2(kc + 1, (kc + 1) & 1);
+    sched_fence();
+    const int q = kc % (PF + 1), qb = kc & 1;
 #pragma unroll
-    for (int pb = 0; pb < 2; ++pb) {
-      const int o = swz(kc * P + pb * 16 + col, g);
-      const f16x8 bh = *reinterpret_cast<const f16x8 *>(Dh + o);
-      const f16x8 bl = *reinterpret_cast<const f16x8 *>(Dl + o);
+    for (int pb = 0; pb < PB; ++pb) {
 #pragma unroll
       for (int j = 0; j < NTW; ++j) {
-        am[j][pb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[q][j], bh, am[j][pb], 0, 0, 0);
-        ac[j][pb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[q][j], bl, ac[j][pb], 0, 0, 0);
-        ac[j][pb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[q][j], bh, ac[j][pb], 0, 0, 0);
+        am[j][pb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[q][j], rbh[qb][pb], am[j][pb], 0, 0, 0);
+        ac[j][pb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[q][j], rbl[qb][pb], ac[j][pb], 0, 0, 0);
+        ac[j][pb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[q][j], rbh[qb][pb], ac[j][pb], 0, 0, 0);
       }
     }
   }
@@ -373,7 +401,7 @@ __global__ void __launch_bounds__(kNT) sldc_kernel(DP p) {
   const __amdgpu_buffer_rsrc_t rr = rsrc(p.r + p.rco, p.rbytes);
   const __amdgpu_buffer_rsrc_t yr = rsrc(p.y + p.yco, p.ybytes);
 #pragma unroll
-  for (int pb = 0; pb < 2; ++pb) {
+  for (int pb = 0; pb < PB; ++pb) {
     const int px = pix0 + pb * 16 + col;
     const bool ok = px < p.npix;
     f32x4 rv[NTW];
@@ -395,27 +423,28 @@ __global__ void __launch_bounds__(kNT) sldc_kernel(DP p) {
   }
 }
 
-template <int C>
+template <int C, int PB>
 int run_dc(DP p, hipStream_t st) {
-  const size_t lds = (size_t)2 * (C / 32) * P * 32 * 2 + (size_t)11 * C * 4;
+  constexpr int PX = 16 * PB;
+  const size_t lds = (size_t)2 * (C / 32) * PX * 32 * 2 + (size_t)11 * C * 4;
   if (lds > 160 * 1024) return DCVC_HIP_EUNSUPPORTED;
-  const int G = (p.npix + P - 1) / P;
-  auto kern = sldc_kernel<C>;
-  dcvc_note_kernel("sldc_kernel<%d>@%lld", C, (long long)G * kNT);
+  const int G = (p.npix + PX - 1) / PX;
+  auto kern = sldc_kernel<C, PB>;
+  dcvc_note_kernel("sldc_kernel<%d, %d>@%lld", C, PB, (long long)G * kNT);
   dcvc_ensure_lds(reinterpret_cast<const void *>(kern), 160 * 1024);
   hipLaunchKernelGGL(kern, dim3((unsigned)G), dim3(kNT), lds, st, p);
   DCVC_LAUNCH_CHECK();
   return DCVC_HIP_OK;
 }
 
-template <int C>
+template <int C, int PB>
 int run(LP p, hipStream_t st) {
-  constexpr int KC = C / 32;
-  const size_t lds = (size_t)2 * KC * P * 32 * 2 + (size_t)4 * 2 * P * 32 * 2 + (size_t)(p.hidden + 2 * C) * 4;
+  constexpr int KC = C / 32, PX = 16 * PB;
+  const size_t lds = (size_t)2 * KC * PX * 32 * 2 + (size_t)4 * 2 * PX * 32 * 2 + (size_t)(p.hidden + 2 * C) * 4;
   if (lds > 160 * 1024) return DCVC_HIP_EUNSUPPORTED;
-  const int G = (p.npix + P - 1) / P;
-  auto kern = slffn_kernel<C>;
-  dcvc_note_kernel("slffn_kernel<%d>@%lld", C, (long long)G * kNT);
+  const int G = (p.npix + PX - 1) / PX;
+  auto kern = slffn_kernel<C, PB>;
+  dcvc_note_kernel("slffn_kernel<%d, %d>@%lld", C, PB, (long long)G * kNT);
   dcvc_ensure_lds(reinterpret_cast<const void *>(kern), 160 * 1024);
   hipLaunchKernelGGL(kern, dim3((unsigned)G), dim3(kNT), lds, st, p);
   DCVC_LAUNCH_CHECK();
@@ -489,7 +518,7 @@ extern "C" int dcvc_internal_lffn(const dcvc_ffn_args *a, void *stream) {
   p.hidden = a->hidden;
   p.slope = a->slope;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  return a->c == 384 ? run<384>(p, st) : run<192>(p, st);
+  return a->c == 384 ? run<384, SLFFN_PB384>(p, st) : run<192, 2>(p, st);
 }
 
 // MFMA A-fragment packing of an R x K fp32 matrix (R % 16 == 0, K % 32 ==
@@ -539,5 +568,5 @@ extern "C" int dcvc_dw_conv2_split(const dcvc_dwc_args *a, void *stream) {
   p.w2bytes = (int)((int64_t)c * c * 2 * 2);
   p.b2 = a->b2;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  return c == 384 ? run_dc<384>(p, st) : c == 192 ? run_dc<192>(p, st) : run_dc<128>(p, st);
+  return c == 384 ? run_dc<384, SLDC_PB384>(p, st) : c == 192 ? run_dc<192, 2>(p, st) : run_dc<128, 2>(p, st);
 }

@@ -1121,6 +1121,7 @@ extern "C" int dcvc_internal_xconv_stamps(unsigned *host) {
 #endif
 }
 extern "C" void dcvc_internal_sconv_dbg(int v);
+extern "C" void dcvc_internal_wconv_dbg(int v);
 extern "C" void dcvc_internal_sconv_rw(int v);
 
 // the split-precision kernels' A/B and timing-ablation options (dcvc_set_option)
@@ -1129,6 +1130,7 @@ extern "C" int dcvc_internal_set_option_split(const char *name, int value) {
   else if (std::strcmp(name, "sconv_rw") == 0) dcvc_internal_sconv_rw(value);
   else if (std::strcmp(name, "xconv_dbg") == 0) g_dbg = value;
   else if (std::strcmp(name, "xconv_rw1") == 0) g_rw1 = value;
+  else if (std::strcmp(name, "wconv_dbg") == 0) dcvc_internal_wconv_dbg(value);
   else return DCVC_HIP_EINVAL;
   return DCVC_HIP_OK;
 }

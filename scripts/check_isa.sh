@@ -37,9 +37,9 @@ for o in "$@"; do
   # the split-precision kernels written since (dconv, sffn): no scratch at
   # all (a private array the compiler could not keep in registers made one
   # dconv build 9x slower, profiles/r05h_micro.jsonl)
-  s=$(awk '/^[0-9a-f]+ <.*(dconv_kernel|sffn_kernel)/{k=1; next} /^[0-9a-f]+ </{k=0} k && /scratch_/' "$T/$n.s" | wc -l)
+  s=$(awk '/^[0-9a-f]+ <.*(dconv_kernel|sffn_kernel|wconv3_kernel)/{k=1; next} /^[0-9a-f]+ </{k=0} k && /scratch_/' "$T/$n.s" | wc -l)
   if [ "$s" != "0" ]; then
-    echo "check_isa: $o has $s scratch instructions in dconv / sffn kernels" >&2
+    echo "check_isa: $o has $s scratch instructions in dconv / sffn / wconv kernels" >&2
     bad=1
   fi
 done

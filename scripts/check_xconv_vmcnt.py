@@ -29,19 +29,21 @@ import tempfile
 
 LLVM = "/opt/rocm/lib/llvm/bin"
 MANGLED = re.compile(r"xconv3_kernelILi(\d+)ELi(\d+)ELi(\d+)ELi(\d+)ELi(\d+)ELb(\d)ELi(\d+)E")
+WMANGLED = re.compile(r"wconv3_kernelILi(\d+)ELi(\d+)ELi(\d+)E")
 
 
-def schedules(lib_path):
+def schedules(lib_path, sym="dcvc_internal_xconv_schedule", nprm=6):
     """{(cin, bn, rw, nw, nres, ks): [(ops, wait)] per stage} of every
-    instantiation the library registered."""
+    instantiation the library registered (wconv.hip's: {(cin, bn, nres): ..},
+    its producer waves' schedule)."""
     lib = ctypes.CDLL(os.path.abspath(lib_path))
-    f = lib.dcvc_internal_xconv_schedule
+    f = getattr(lib, sym)
     f.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_int), ctypes.c_char_p, ctypes.c_int]
     f.restype = ctypes.c_int
     out = {}
     i = 0
     while True:
-        prm = (ctypes.c_int * 6)()
+        prm = (ctypes.c_int * nprm)()
         buf = ctypes.create_string_buffer(1 << 16)
         if f(i, prm, buf, len(buf)) != 0:
             break
@@ -70,14 +72,14 @@ def disassemble(obj):
                               text=True).stdout
 
 
-def kernels(listing):
+def kernels(listing, tag="xconv3_kernel"):
     """{mangled name: [(address, mnemonic, operands, branch target or None)]}
-    of the xconv3_kernel functions."""
+    of the xconv3_kernel (or tag) functions."""
     out, cur, base = {}, None, 0
     for ln in listing.splitlines():
         m = re.match(r"^([0-9a-f]+) <(.*)>:", ln)
         if m:
-            cur = m.group(2) if "xconv3_kernel" in m.group(2) else None
+            cur = m.group(2) if tag in m.group(2) else None
             base = int(m.group(1), 16)
             if cur:
                 out[cur] = []
@@ -111,7 +113,7 @@ def vmcnt_of(ops):
     return int(m.group(1)) if m else None
 
 
-def check_kernel(name, ins, sched):
+def check_kernel(name, ins, sched, dma_loop=False):
     """Errors and notes for one instantiation.
 
     The tile loop is the address range from the target of its back-edges to
@@ -126,11 +128,21 @@ def check_kernel(name, ins, sched):
     back = [(a, t) for a, mn, _, t in ins if t is not None and t < a]
     if not back:
         return [f"{name}: no loop back-edge"], notes
-    # (the last back-edge is the tile loop's; small loops before it, such as
-    # the prologue's bias copy, lie outside its range)
-    end, top = max(back)
+    if dma_loop:
+        # wconv3_kernel: the producer waves' tile loop is the one that issues
+        # the weight LDS-DMAs (the consumer loop, after it, issues none)
+        cand = [(a, t) for a, t in back
+                if any(kind(mn, o) == "D" for x, mn, o, _ in ins if t <= x <= a)]
+        if not cand:
+            return [f"{name}: no loop issues a weight LDS-DMA"], notes
+        end, top = max(cand, key=lambda e: e[0] - e[1])
+        outside = ""
+    else:
+        # (the last back-edge is the tile loop's; small loops before it, such
+        # as the prologue's bias copy, lie outside its range)
+        end, top = max(back)
+        outside = "".join(c for c in (kind(mn, ops) for a, mn, ops, _ in ins if a > end) if c and c != "S")
     body = [(a, mn, ops) for a, mn, ops, _ in ins if top <= a <= end]
-    outside = "".join(c for c in (kind(mn, ops) for a, mn, ops, _ in ins if a > end) if c and c != "S")
     bars = [i for i, (_, mn, _) in enumerate(body) if mn == "s_barrier"]
     if len(bars) != nb:
         return [f"{name}: {len(bars)} barriers in the tile loop, the schedule has {nb} stage barriers"], notes
@@ -182,8 +194,11 @@ def main(argv):
     if len(argv) != 3:
         print(__doc__)
         return 2
+    listing = disassemble(argv[2])
+    if "wconv3_kernel" in listing:
+        return main_wconv(argv[1], listing)
     sched = schedules(argv[1])
-    ks = kernels(disassemble(argv[2]))
+    ks = kernels(listing)
     if not ks:
         print("check_xconv_vmcnt: no xconv3_kernel in", argv[2], file=sys.stderr)
         return 1
@@ -209,6 +224,30 @@ def main(argv):
     if errs:
         return 1
     print(f"check_xconv_vmcnt: {seen} xconv3_kernel instantiations match their vmcnt schedules")
+    return 0
+
+
+def main_wconv(lib, listing):
+    """wconv.hip's object: the producer loop of every wconv3_kernel."""
+    sched = schedules(lib, "dcvc_internal_wconv_schedule", 3)
+    errs, notes, seen = [], [], 0
+    for name, ins in sorted(kernels(listing, "wconv3_kernel").items()):
+        m = WMANGLED.search(name)
+        key = tuple(int(v) for v in m.groups()) if m else None
+        if key not in sched:
+            errs.append(f"{name}: no schedule registered for {key}")
+            continue
+        e, n = check_kernel("wconv3_kernel<%d,%d,%d>" % key, ins, sched[key], dma_loop=True)
+        errs += e
+        notes += n
+        seen += 1
+    for n in notes:
+        print("check_xconv_vmcnt: note:", n)
+    for e in errs:
+        print("check_xconv_vmcnt:", e, file=sys.stderr)
+    if errs or not seen:
+        return 1
+    print(f"check_xconv_vmcnt: {seen} wconv3_kernel instantiations match their vmcnt schedules")
     return 0
 
 
