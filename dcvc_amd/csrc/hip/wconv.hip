@@ -595,12 +595,17 @@ wconv3_kernel(WP p) {
             read_b(std::integral_constant<int, s1>{}, std::integral_constant<int, 0>{}, ib1,
                    std::integral_constant<int, q ^ 1>{});
           if (WDBG(1)) return;
+          // (two passes, so the two products accumulated into ac[r][j] sit
+          // 2 NT - 1 MFMAs apart: none waits on its predecessor's result;
+          // the accumulation order, and so the bits, are unchanged)
 #pragma unroll
           for (int j = 0; j < NT; ++j) {
             am[r][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(oa[S][j][0], ob[q][0], am[r][j], 0, 0, 0);
             ac[r][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(oa[S][j][0], ob[q][1], ac[r][j], 0, 0, 0);
-            ac[r][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(oa[S][j][1], ob[q][0], ac[r][j], 0, 0, 0);
           }
+#pragma unroll
+          for (int j = 0; j < NT; ++j)
+            ac[r][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(oa[S][j][1], ob[q][0], ac[r][j], 0, 0, 0);
         });
         if constexpr (s == NST - 1) {
           if (!WDBG(64)) epilogue(tc);

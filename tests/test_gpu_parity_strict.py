@@ -405,9 +405,11 @@ def test_hem_c1_estimate_teacher_forced(prec):
     pair = HemPair(g.i_state_dict(), g.p_state_dict(), g.q("C1"), prec)
     qi, qmv, qy = g.q("C1")
     dpb_o, rows = None, []
-    # the fixture's estimates were made at 8 CPU threads: the oracle runs at
-    # that count so that its float sums (and its rounding ties) are the
-    # reference's (at 16 threads one P-frame's estimate moved 4e-4)
+    # the fixture's estimates were made at 8 CPU threads; the oracle runs at
+    # that count too, but its float sums also follow the CPU's vector width, so
+    # on another machine a rounding tie can still fall the other way: on the
+    # GPU box frame 2's oracle estimate sat 4.1e-4 from the reference's and
+    # frame 3's reference 3.0e-4 from the oracle's
     nthr = torch.get_num_threads()
     torch.set_num_threads(8)
     with torch.no_grad():
@@ -442,7 +444,11 @@ def test_hem_c1_estimate_teacher_forced(prec):
         # estimated bits are sums of -log2 p over every element: a symbol or
         # index flipped at a rounding tie (the ties tests/parity.py admits)
         # moves a frame's estimate by a few bits to tens of bits (3e-5 of it
-        # seen in split precision)
-        assert abs(s["bit"] - s["bit_oracle"]) / s["bit_oracle"] < 1e-4, s
+        # seen in split precision).  The product must sit within 1e-4 of one
+        # of the two CPU computations of the frame, the oracle's or the
+        # reference's own (which differ at such ties by up to 4e-4, above);
+        # measured: within 2e-7 of one of them on every frame
+        d = min(abs(s["bit"] - s["bit_oracle"]), abs(s["bit"] - s["bit_ref"]))
+        assert d / s["bit_ref"] < 1e-4, s
         assert abs(s["bit_oracle"] - s["bit_ref"]) / s["bit_ref"] < 1e-3, s
         assert abs(s["psnr"] - s["psnr_oracle"]) < 1e-4, s
