@@ -158,6 +158,11 @@ def lib():
     global _L
     if _L is None:
         _L = hip_lib()
+        # DCVC_HIP_OPTIONS="name=v,name=v": dcvc_set_option switches applied at
+        # load (whole-bench kernel A/B runs, e.g. "wconv=1"); unset in production
+        for kv in filter(None, os.environ.get("DCVC_HIP_OPTIONS", "").split(",")):
+            k, _, v = kv.partition("=")
+            check(_L.dcvc_set_option(k.strip().encode(), int(v)), "set_option")
     return _L
 
 
