@@ -46,7 +46,7 @@ STRICT_TESTS = {("dc", False): ("tests/test_gpu_parity_strict.py::test_strict_pa
                 ("hem", False): ("tests/test_gpu_parity_strict.py::test_strict_parity_hem_c2_1080p",
                                  "I + P frames at 1920x1080"),
                 ("dc", True): ("tests/test_gpu_parity_strict.py::test_strict_parity_c4_yuv420",
-                               "I-frame at 3840x2160, I + P frames at 1920x1080")}
+                               "I + P frames at 3840x2160 and at 1920x1080")}
 
 
 def parity_evidence(args, parity):
