@@ -46,7 +46,7 @@ constexpr int HS = 64;    // hidden channels per slice (4 row blocks: one per wa
 // fragments at C = 384) from L2 into registers; 4 blocks halve those L2
 // bytes per pixel and the grid, but measured 100 vs 60 us (sldc 59 vs 34 us,
 // profiles/r06c_latent_pb_ab.jsonl): the time follows the MFMAs of its one
-// wave per SIMD, not the L2 bytes, so 2 stays (DESIGN.md section 9.0).
+// wave per SIMD, not the L2 bytes, so 2 stays (DESIGN.md section 9.R6).
 #ifndef SLFFN_PB384
 #define SLFFN_PB384 2
 #endif
