@@ -72,7 +72,17 @@ struct GG {
   static_assert((PD - 1) * L < 64, "vmcnt is 6 bits");
 };
 
-constexpr int kOob = 0x7fffffe0;   // a buffer offset past any num_records: the load returns zeros
+constexpr int kOob = 0x7fffffe0;
+
+// f(integral_constant<int, I>) for I = 0 .. N - 1, in order
+template <typename F, int... I>
+__device__ __forceinline__ void sfor_(F &&f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, typename F>
+__device__ __forceinline__ void sfor(F &&f) {
+  sfor_(f, std::make_integer_sequence<int, N>{});
+}   // a buffer offset past any num_records: the load returns zeros
 
 template <int BN, int PXW, int PD, bool GATE>
 __global__ void __launch_bounds__(256) sgemm_kernel(GP p) {
@@ -126,19 +136,42 @@ __global__ void __launch_bounds__(256) sgemm_kernel(GP p) {
     const int lp = (wave * PXW + r) * 16 + dpx;
     xoff[r] = pix0 + lp < p.npix ? (lp * p.xcs + dls * 4) * 4 : -1;
   }
+  // per-lane parts of every LDS-DMA offset, computed once: a stage adds its
+  // chunk's uniform offset (s * wchunk halves of weights, 32 channels of
+  // pixels) and compares the chunk against per-lane limits (weights: the
+  // chunk count and cout; pixels: cin), so a stage's address work is an add
+  // and a select per DMA instead of its 64-bit index arithmetic
+  int wbase[DPW];
+  bool wok[DPW];
+#pragma unroll
+  for (int d = 0; d < DPW; ++d) {
+    const int i = wave + 4 * d;
+    const int hl = i >= BN / 16, k = hl ? i - BN / 16 : i;
+    const int R = k * 16 + dpx;
+    const int ls = (lane & 3) ^ ((0x1320 >> (((R >> 2) & 3) << 2)) & 3);
+    const int n = n0 + R;
+    wok[d] = n < p.cout;
+    wbase[d] = ((hl ? p.cout * 32 : 0) + n * 32 + ls * 8) * 2;
+  }
+  const int wcb = (int)(p.wchunk * 2);
+  int xbase[G_::NX][PXW][2], xlim[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) xlim[h] = p.cin - h * 16 - dls * 4;   // chunk s reads channel s * 32 + (cin - xlim)
+#pragma unroll
+  for (int gx = 0; gx < G_::NX; ++gx)
+#pragma unroll
+    for (int r = 0; r < PXW; ++r)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) xbase[gx][r][h] = xoff[r] >= 0 ? xoff[r] + (h * 16 + gx * p.cin) * 4 : -1;
   auto issue = [&](int s, int b) {
     uint16_t *Lb = Ls + (size_t)b * SH;
-    const int64_t cbase = (int64_t)s * p.wchunk;
+    const bool live = s < p.nchunks;
+    const int wso = live ? s * wcb : 0, xso = s * 128, c0 = s * 32;
 #pragma unroll
     for (int d = 0; d < DPW; ++d) {
       const int i = wave + 4 * d;
       const int hl = i >= BN / 16, k = hl ? i - BN / 16 : i;
-      const int R = k * 16 + dpx;
-      const int ls = (lane & 3) ^ ((0x1320 >> (((R >> 2) & 3) << 2)) & 3);
-      const int n = n0 + R;
-      const int voff = (s < p.nchunks && n < p.cout)
-                           ? (int)((cbase + (hl ? (int64_t)p.cout * 32 : 0) + (int64_t)n * 32 + ls * 8) * 2)
-                           : kOob;
+      const int voff = live && wok[d] ? wbase[d] + wso : kOob;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(
           wr, (__attribute__((address_space(3))) void *)(Lb + hl * (WH / 2) + k * 512), 16, voff, 0, 0, 0);
     }
@@ -148,8 +181,7 @@ __global__ void __launch_bounds__(256) sgemm_kernel(GP p) {
       for (int r = 0; r < PXW; ++r)
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
-          const int c = s * 32 + h * 16 + dls * 4;
-          const int o = (xoff[r] >= 0 && c < p.cin) ? xoff[r] + (s * 32 + h * 16 + gx * p.cin) * 4 : kOob;
+          const int o = (xbase[gx][r][h] >= 0 && c0 < xlim[h]) ? xbase[gx][r][h] + xso : kOob;
           __builtin_amdgcn_raw_ptr_buffer_load_lds(
               xr, (__attribute__((address_space(3))) void *)(Lb + WH + gx * (BM * 64) + ((wave * PXW + r) * 2 + h) * 512),
               16, o, 0, 0, 0);
@@ -169,14 +201,17 @@ __global__ void __launch_bounds__(256) sgemm_kernel(GP p) {
   for (int j = 0; j < PD; ++j) issue(j, j);
   const int nst = p.nchunks;
   const bool lrelu = p.in_op == DCVC_IN_LRELU;
-  for (int s = 0; s < nst; ++s) {
+  // one 32-channel stage on stage buffer B (compile-time: the loop below runs
+  // the NB buffers in turn, so every LDS address is an immediate offset)
+  auto stage = [&](int s, auto B_) {
+    constexpr int B = decltype(B_)::value;
     // stage s's pieces (issued PD stages ago) have landed for this wave; the
     // barrier makes every wave's pieces visible and retires stage s - 1's
     // reads of the buffer the next issue refills
     wait_vm_n_lgkm<(PD - 1) * L>();
     raw_barrier();
-    issue(s + PD, (s + PD) % NB);
-    const uint16_t *Lb = Ls + (size_t)(s % NB) * SH;
+    issue(s + PD, (B + PD) % NB);
+    const uint16_t *Lb = Ls + (size_t)B * SH;
     f16x8 bh[PXW], bl[PXW];
 #pragma unroll
     for (int r = 0; r < PXW; ++r) {
@@ -203,8 +238,10 @@ __global__ void __launch_bounds__(256) sgemm_kernel(GP p) {
           v[4 + e] = v[4 + e] * g1;
         }
       } else if (lrelu) {
+        // (max(v, s v): the host admits 0 <= s <= 1 only, where it is the
+        // leaky ReLU, signed zeros included)
 #pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] = v[e] >= 0.f ? v[e] : v[e] * p.in_slope;
+        for (int e = 0; e < 8; ++e) v[e] = lrelu_in(v[e], p.in_slope);
       }
       u32x4_t h, l;
       rg.add8(v);
@@ -212,19 +249,30 @@ __global__ void __launch_bounds__(256) sgemm_kernel(GP p) {
       bh[r] = __builtin_bit_cast(f16x8, h);
       bl[r] = __builtin_bit_cast(f16x8, l);
     }
+    // (the second ac product of every (r, jn) after all the first ones: no
+    // MFMA waits on its predecessor's result; the same accumulation order)
+    f16x8 al[NT];
 #pragma unroll
     for (int jn = 0; jn < NT; ++jn) {
       const int o = swz(jn * 16 + col, hi);
       const f16x8 ah = *reinterpret_cast<const f16x8 *>(Lb + o);
-      const f16x8 al = *reinterpret_cast<const f16x8 *>(Lb + WH / 2 + o);
+      al[jn] = *reinterpret_cast<const f16x8 *>(Lb + WH / 2 + o);
 #pragma unroll
       for (int r = 0; r < PXW; ++r) {
         am[r][jn] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh[r], am[r][jn], 0, 0, 0);
         ac[r][jn] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bl[r], ac[r][jn], 0, 0, 0);
-        ac[r][jn] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh[r], ac[r][jn], 0, 0, 0);
       }
     }
-  }
+#pragma unroll
+    for (int jn = 0; jn < NT; ++jn)
+#pragma unroll
+      for (int r = 0; r < PXW; ++r)
+        ac[r][jn] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[jn], bh[r], ac[r][jn], 0, 0, 0);
+  };
+  for (int s = 0; s < nst; s += NB)
+    sfor<NB>([&](auto B_) {
+      if (s + decltype(B_)::value < nst) stage(s + decltype(B_)::value, B_);
+    });
   wait_vm_lgkm();   // the zero-fill pieces past the last stage: no LDS-DMA in flight at exit
 
   if (p.shuffle) {
@@ -388,6 +436,8 @@ extern "C" int dcvc_internal_sgemm(const dcvc_conv_args *a, void *stream) {
   if (a->kh != 1 || a->kw != 1 || a->stride != 1 || a->pad != 0) return DCVC_HIP_EUNSUPPORTED;
   const bool gate = a->in_op == DCVC_IN_GATE;
   if (a->in_op != DCVC_IN_NONE && a->in_op != DCVC_IN_LRELU && !(gate && g_gate)) return DCVC_HIP_EUNSUPPORTED;
+  // (the kernel's input leaky ReLU is max(v, s v): 0 <= s <= 1)
+  if (a->in_op == DCVC_IN_LRELU && !(a->in_slope >= 0.f && a->in_slope <= 1.f)) return DCVC_HIP_EUNSUPPORTED;
   if (gate && a->shuffle) return DCVC_HIP_EUNSUPPORTED;
   if (a->x.dtype != DCVC_F32 || a->y.dtype != DCVC_F32) return DCVC_HIP_EUNSUPPORTED;
   const int f = a->shuffle ? 2 : 1;
