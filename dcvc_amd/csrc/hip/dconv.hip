@@ -142,6 +142,26 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
   // the (tile, K step) whose operands load next, wave-uniform: tile ta at
   // output row ly, first column lx; step = chunk lc, row lr of the chunk
   int ta = t, ly = t / p.nseg, lx = (t - ly * p.nseg) * (16 * NP), lc = 0, lr = 0;
+  // 1x1 layers: the one tap's input pixel of each lane's output pixels, as a
+  // byte offset (-1 outside the tile / image), set once per tile, so a K
+  // step's address is that plus its channel offset (the generic path below
+  // recomputes the pixel index, a per-lane multiply by the channel stride,
+  // every step)
+  int obase[NP];
+  auto setup = [&]() __attribute__((always_inline)) {
+    if constexpr (KS == 1) {
+      const int iy = ly * p.S - p.pad;
+      const bool rowok = ta < p.ntiles && (unsigned)iy < (unsigned)p.H;
+#pragma unroll
+      for (int j = 0; j < NP; ++j) {
+        const int ox = lx + j * 16 + col;
+        const int ix = ox * p.S - p.pad;
+        const bool ok = rowok && (unsigned)ix < (unsigned)p.W && ox < p.Wo;
+        obase[j] = ok ? ((iy * p.W + ix) * p.xcs + p.xco) * 4 : -1;
+      }
+    }
+  };
+  setup();
   auto next = [&]() __attribute__((always_inline)) {
     ++lr;
     if (lc < p.nch - 1 && lr == p.kt) {
@@ -153,6 +173,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
       ta += GW;
       ly = ta / p.nseg;
       lx = (ta - ly * p.nseg) * (16 * NP);
+      setup();
     }
   };
   // B-operand raw loads of the next (tile, step) into pr (GATE: the gate
@@ -170,12 +191,20 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
     const int dy = tap / KS, dx = tap - dy * KS;
     const int iy = ly * p.S + dy - p.pad;
     const bool rowok = ta < p.ntiles && tap < p.kt && ch < p.cin && (unsigned)iy < (unsigned)p.H;
+    const bool chok = tap < p.kt && ch < p.cin;
 #pragma unroll
     for (int j = 0; j < NP; ++j) {
-      const int ox = lx + j * 16 + col;
-      const int ix = ox * p.S + dx - p.pad;
-      const bool ok = rowok && (unsigned)ix < (unsigned)p.W && ox < p.Wo;
-      const int o = ok ? ((iy * p.W + ix) * p.xcs + p.xco + ch) * 4 : 0x7fffffe0;
+      int o;
+      bool ok;
+      if constexpr (KS == 1) {
+        ok = chok && obase[j] >= 0;
+        o = ok ? obase[j] + ch * 4 : 0x7fffffe0;
+      } else {
+        const int ox = lx + j * 16 + col;
+        const int ix = ox * p.S + dx - p.pad;
+        ok = rowok && (unsigned)ix < (unsigned)p.W && ox < p.Wo;
+        o = ok ? ((iy * p.W + ix) * p.xcs + p.xco + ch) * 4 : 0x7fffffe0;
+      }
       const f32x4 a = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, o, 0, 0));
       const f32x4 b = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, o + 16, 0, 0));
 #pragma unroll
