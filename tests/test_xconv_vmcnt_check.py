@@ -61,3 +61,16 @@ def test_dead_load_count_fails(toolchain, tmp_path):
     # the tile's first stages load the 16-channel last chunk: 2 pieces (4
     # loads) emitted, round 5's count assumed 3 (6)
     assert "vector-memory instructions DLLLLD, the vmcnt schedule assumes DLLLLLLD" in r.stderr, r.stderr
+
+
+def test_built_wconv_matches_its_schedule(toolchain):
+    """wconv.hip's DMA wave (the only waves that issue LDS-DMAs and wait with
+    exact vmcnt counts) in the built library: every instantiation's DMA loop
+    issues exactly the schedule dcvc_internal_wconv_schedule reports."""
+    lib = os.path.join(REPO, "dcvc_amd/lib/libdcvc_hip.so")
+    obj = os.path.join(REPO, "build/hip/wconv.o")
+    if not (os.path.exists(lib) and os.path.exists(obj)):
+        pytest.skip("library not built (make hip)")
+    r = _check(lib, obj)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "16 wconv3_kernel instantiations match" in r.stdout
