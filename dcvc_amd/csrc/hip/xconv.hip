@@ -563,9 +563,6 @@ xconv3_kernel(XP p) {
   // the lane's output pieces: pixel (row wave * RW + r, column col), channels
   // n0 + 16 j + 4 hi .. + 3; offsets in elements from the tile's first output
   // pixel.  Full tiles (every piece inside the output) skip the tests
-  auto piece_ok = [&](const TI &ti, int r, int j) {
-    return ti.oy0 + wave * RW + r < p.Ho && ti.ox0 + col < p.Wo && ti.n0 + j * 16 + hi * 4 < p.cout;
-  };
   auto full_tile = [&](const TI &ti) {
     return ti.oy0 + G::TH <= p.Ho && ti.ox0 + 16 <= p.Wo && ti.n0 + BN <= p.cout;
   };
