@@ -38,6 +38,12 @@
 #include <string>
 #include <utility>
 
+// consumer (MFMA) waves: 4 (one per SIMD, 4 rows each) or 8 (two per SIMD,
+// 2 rows each; 12 waves in all, 3 per SIMD)
+#ifndef WCONV_NC
+#define WCONV_NC 4
+#endif
+
 namespace {
 
 struct WP {
@@ -92,11 +98,13 @@ struct WG {
   // and xconv.hip) every weight wait also waited for the image loads issued
   // before it -- a 50 us share of 397 us at 48 -> 48 1080p in the timing
   // ablation (profiles/r06g_wconv_ablation.jsonl)
-  static constexpr int KS = 3, KT = 9, NC = 4, NIW = 3, NDW = 1, NT = BN / 16;
+  static constexpr int KS = 3, KT = 9, NC = WCONV_NC, NIW = 3, NDW = 1, NT = BN / 16;
+  static constexpr int NTH = (NC + NDW + NIW) * 64;         // threads (the kernel's launch bound: (WCONV_NC + 4) * 64)
+  static_assert(NDW + NIW == 4, "launch bound");
   // rows per consumer wave: 4, or 3 for 48-channel n-blocks with a residual
   // (the residual's 12 fragments on top of 24 accumulator pairs and two
   // operand sets would not fit the 256 registers of 2 waves / SIMD)
-  static constexpr int RW = NRES >= 1 && NT == 3 ? 3 : 4, TH = NC * RW;
+  static constexpr int RW = NC == 8 ? 2 : (NRES >= 1 && NT == 3 ? 3 : 4), TH = NC * RW;
   static constexpr int PT = NIW * 64;                      // image-producer threads
   static constexpr int IH = TH + 2, IW = 18, IWP = 20;
   static constexpr int CH = (CIN + 31) / 32;
@@ -155,7 +163,8 @@ struct WG {
 };
 
 template <int CIN, int BN, int NRES>
-__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2)))
+__global__ void __launch_bounds__((WCONV_NC + 4) * 64)
+    __attribute__((amdgpu_waves_per_eu(WCONV_NC == 8 ? 3 : 2, WCONV_NC == 8 ? 3 : 2)))
 wconv3_kernel(WP p) {
   typedef WG<CIN, BN, NRES> G;
   constexpr int NT = G::NT, RW = G::RW, IH = G::IH, IW = G::IW, IWP = G::IWP, IMG = G::IMG, WST = G::WST;
@@ -176,7 +185,7 @@ wconv3_kernel(WP p) {
   if ((GR & 7) == 0) g = (g & 7) * (GR >> 3) + (g >> 3);   // consecutive tiles on one XCD
   if (g >= p.ntiles) return;
 
-  for (int i = tid; i < p.cout; i += 512) {
+  for (int i = tid; i < p.cout; i += G::NTH) {
     Lc[i] = p.bias ? p.bias[i] : 0.f;
     Lc[p.cout + i] = p.scale ? p.scale[i] : 1.f;
   }
@@ -674,9 +683,9 @@ int launch(WP p, hipStream_t st) {
   int64_t grid = g_cus;
   if (grid > nt) grid = nt;
   auto kern = wconv3_kernel<CIN, BN, NRES>;
-  dcvc_note_kernel("wconv3_kernel<%d, %d, %d>@%lld", CIN, BN, NRES, (long long)grid * 512);
+  dcvc_note_kernel("wconv3_kernel<%d, %d, %d>@%lld", CIN, BN, NRES, (long long)grid * G::NTH);
   dcvc_ensure_lds(reinterpret_cast<const void *>(kern), 160 * 1024);
-  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(512), lds, st, p);
+  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(G::NTH), lds, st, p);
   DCVC_LAUNCH_CHECK();
   return DCVC_HIP_OK;
 }
