@@ -44,7 +44,8 @@ build/hip/%.o: dcvc_amd/csrc/hip/%.hip $(HIP_HDRS)
 
 # check_isa.sh: no packed-f32 VALU, no scratch in the split kernels;
 # check_xconv_vmcnt.py: every xconv3_kernel instantiation issues exactly the
-# vector-memory instructions its exact vmcnt waits count (the library is
+# vector-memory instructions its exact vmcnt waits count, and so do
+# wconv3_kernel's DMA wave and the streamed sffn_kernels (the library is
 # linked to a temporary name first and only kept if the check passes)
 $(LIB)/libdcvc_hip.so: $(HIP_OBJS) scripts/check_isa.sh scripts/check_xconv_vmcnt.py
 	@mkdir -p $(LIB)
@@ -52,6 +53,7 @@ $(LIB)/libdcvc_hip.so: $(HIP_OBJS) scripts/check_isa.sh scripts/check_xconv_vmcn
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@.tmp $(HIP_OBJS)
 	$(PYTHON) scripts/check_xconv_vmcnt.py $@.tmp build/hip/xconv.o || { rm -f $@.tmp; exit 1; }
 	$(PYTHON) scripts/check_xconv_vmcnt.py $@.tmp build/hip/wconv.o || { rm -f $@.tmp; exit 1; }
+	$(PYTHON) scripts/check_xconv_vmcnt.py $@.tmp build/hip/sffn.o || { rm -f $@.tmp; exit 1; }
 	mv $@.tmp $@
 
 oracle/_build/liboracle_rans.so: oracle/rans_oracle.c

@@ -30,6 +30,7 @@
 #include "common.h"
 #include "split.h"
 
+#include <type_traits>
 #include <utility>
 
 namespace {
@@ -212,11 +213,12 @@ sffn_kernel(FP p) {
   // the DMA of slice s + 2 (into that buffer) is issued right after it, and
   // B_s waits for slice s's DMA (issued at B_(s-2)): younger than it are
   // slice s + 1's DMA and, at B_1 and B_2, the next tile's input prefetch
-  // (issued after B_0's DMA)
+  // (issued after B_0's DMA; on the last tile too, all of it out of range,
+  // so that the counts are fixed).  pf: std::true_type at B_1 and B_2
   static_assert(G_::RES || (NS % NB == 0 && NB == 4), "streamed: four buffers, slices a multiple of them");
-  auto barrier_w = [&](int s, bool more) {
+  auto barrier_w = [&](int s, auto pf) {
     if constexpr (!G_::RES) {
-      if ((s == 1 || s == 2) && more) wait_vm_n_lgkm<NDW + G_::PFN>();
+      if constexpr (decltype(pf)::value) wait_vm_n_lgkm<NDW + G_::PFN>();
       else wait_vm_n_lgkm<NDW>();
       raw_barrier();
       issue_w((s + 2) % NS, (s + 2) % NB);
@@ -254,8 +256,9 @@ sffn_kernel(FP p) {
     // to keep) after the tile's last ffn1 instead, into the registers of the
     // input operands, dead by then
     constexpr bool LATE_PF = G_::RES && C == 64;
-    barrier_w(0, more);
-    if (!LATE_PF && more) prefetch(t + G);
+    barrier_w(0, std::false_type{});
+    if constexpr (!G_::RES) prefetch(t + G);
+    else if (!LATE_PF && more) prefetch(t + G);
     ffn1(hA, wslice(0), xh, xl);
     // ffn2 of slice s from the activation of hh
     auto ffn2 = [&](const auto &hh, int s) {
@@ -275,17 +278,26 @@ sffn_kernel(FP p) {
         }
       }
     };
-    static_assert(NS % 2 == 0, "slices come in pairs");
+    static_assert(NS % 2 == 0 && NS >= 4, "slices come in pairs, at least two");
     // two slices an iteration (hA, hB alternate), not unrolled further: the
-    // registers stay those of one pair
+    // registers stay those of one pair.  The first pair is peeled (its
+    // barriers count the prefetch), so no barrier's vmcnt depends on a
+    // runtime condition: the build-time check (scripts/check_xconv_vmcnt.py)
+    // walks every path to each barrier
+    barrier_w(1, std::true_type{});
+    ffn1(hB, wslice(1), xh, xl);
+    ffn2(hA, 0);
+    barrier_w(2, std::true_type{});
+    ffn1(hA, wslice(2), xh, xl);
+    ffn2(hB, 1);
 #pragma unroll 1
-    for (int s = 0; s < NS; s += 2) {
-      barrier_w(s + 1, more);
+    for (int s = 2; s < NS; s += 2) {
+      barrier_w(s + 1, std::false_type{});
       ffn1(hB, wslice(s + 1), xh, xl);
       if (LATE_PF && s + 2 >= NS && more) prefetch(t + G);
       ffn2(hA, s);
       if (s + 2 < NS) {
-        barrier_w(s + 2, more);
+        barrier_w(s + 2, std::false_type{});
         ffn1(hA, wslice(s + 2), xh, xl);
       }
       ffn2(hB, s + 1);

@@ -17,6 +17,11 @@ no GPU) with the instructions in the code object:
   * the vmcnt of the wait in front of each stage barrier must be the
     template's (a smaller one is stricter, reported, not fatal).
 
+The same script checks wconv.hip's object (its DMA wave's loop against
+dcvc_internal_wconv_schedule) and sffn.hip's (the streamed kernels: on every
+control-flow path to a barrier, the slice DMA it waits for is followed by at
+least vmcnt(N) vector-memory instructions; check_sffn_kernel).
+
     python scripts/check_xconv_vmcnt.py dcvc_amd/lib/libdcvc_hip.so build/hip/xconv.o
     python scripts/check_xconv_vmcnt.py LIB disasm.s      (an llvm-objdump -d listing)
 """
@@ -197,6 +202,8 @@ def main(argv):
     listing = disassemble(argv[2])
     if "wconv3_kernel" in listing:
         return main_wconv(argv[1], listing)
+    if "sffn_kernel" in listing:
+        return main_sffn(listing)
     sched = schedules(argv[1])
     ks = kernels(listing)
     if not ks:
@@ -248,6 +255,109 @@ def main_wconv(lib, listing):
     if errs or not seen:
         return 1
     print(f"check_xconv_vmcnt: {seen} wconv3_kernel instantiations match their vmcnt schedules")
+    return 0
+
+
+SMANGLED = re.compile(r"sffn_kernelILi(\d+)ELi(\d+)ELi(\d+)ELi(\d+)E")
+
+
+def sffn_ndw(c, nw):
+    """LDS-DMA instructions per wave per streamed slice (sffn.hip FG::NDW)."""
+    kc1, c16 = (c + 31) // 32, (c + 15) // 16 * 16
+    slice_halves = 2 * kc1 * 32 * 32 + 2 * c16 * 32
+    return slice_halves * 2 // 1024 // nw
+
+
+def successors(ins):
+    """Control-flow successors (indexes) of every instruction."""
+    at = {a: i for i, (a, _, _, _) in enumerate(ins)}
+    out = []
+    for i, (a, mn, _, t) in enumerate(ins):
+        nxt = [i + 1] if i + 1 < len(ins) else []
+        if mn == "s_branch":
+            out.append([at[t]] if t in at else [])
+        elif mn.startswith("s_cbranch"):
+            out.append(([at[t]] if t in at else []) + nxt)
+        elif mn == "s_endpgm" or mn.startswith("s_setpc"):
+            out.append([])
+        else:
+            out.append(nxt)
+    return out
+
+
+def check_sffn_kernel(name, ins, ndw):
+    """Errors for one streamed sffn_kernel.  Barrier B_s waits for slice s's
+    LDS-DMA, issued two barriers earlier (each barrier issues the DMA of the
+    slice two ahead): walking back from B_s's vmcnt(N) wait along any path,
+    the first NDW DMA instructions met are slice s + 1's and the next one is
+    the youngest of slice s's, so at least N vector-memory instructions must
+    lie between it and the wait (then vmcnt(N) covers it).  The walk is over
+    the control-flow graph, so the runtime-selected waits of B_1 / B_2 (the
+    next tile's input prefetch counted or not) are each checked on their own
+    paths, and a prefetch that hipcc hoisted above a DMA shows up."""
+    succ = successors(ins)
+    pred = [[] for _ in ins]
+    for i, ss in enumerate(succ):
+        for j in ss:
+            pred[j].append(i)
+    errs, nbar = [], 0
+    for b, (addr, mn, _, _) in enumerate(ins):
+        if mn != "s_barrier":
+            continue
+        nbar += 1
+        # (index, N or None while looking for the wait, vm ops since the wait, D ops since the wait)
+        best = {}
+        stack = [(p, None, 0, 0) for p in pred[b]]
+        worst = None
+        while stack:
+            i, n, nops, nd = stack.pop()
+            key = (i, n, nd)
+            if key in best and best[key] <= nops:
+                continue
+            best[key] = nops
+            a, m, o, _ = ins[i]
+            k = kind(m, o)
+            if n is None:
+                if m == "s_waitcnt" and vmcnt_of(o) is not None:
+                    n = vmcnt_of(o)
+                elif m == "s_barrier":
+                    errs.append(f"{name}: barrier at {addr:#x}: a path from the barrier at {a:#x} has no vmcnt wait")
+                    continue
+            elif k:
+                if k == "D" and nd == ndw:
+                    if worst is None or nops - n < worst[0]:
+                        worst = (nops - n, nops, n, a)
+                    continue
+                nops += 1
+                nd += k == "D"
+            stack += [(p, n, nops, nd) for p in pred[i]]
+        if worst is not None and worst[0] < 0:
+            errs.append(f"{name}: barrier at {addr:#x}: vmcnt({worst[2]}), but only {worst[1]} vector-memory "
+                        f"instructions follow the DMA it waits for (at {worst[3]:#x}) on some path")
+    if nbar == 0:
+        errs.append(f"{name}: no barrier")
+    return errs, nbar
+
+
+def main_sffn(listing):
+    """sffn.hip's object: every streamed (NBUF > 0) sffn_kernel."""
+    errs, seen = [], 0
+    for name, ins in sorted(kernels(listing, "sffn_kernel").items()):
+        m = SMANGLED.search(name)
+        if not m:
+            errs.append(f"{name}: cannot read the template parameters")
+            continue
+        c, nw, np_, nbuf = (int(v) for v in m.groups())
+        if nbuf == 0:
+            continue   # every slice resident: vmcnt(0) before the one barrier
+        e, nb = check_sffn_kernel(f"sffn_kernel<{c},{nw},{np_},{nbuf}>", ins, sffn_ndw(c, nw))
+        errs += e
+        seen += 1
+    for e in errs:
+        print("check_xconv_vmcnt:", e, file=sys.stderr)
+    if errs or not seen:
+        return 1
+    print(f"check_xconv_vmcnt: {seen} streamed sffn_kernel instantiations wait for each slice's DMA")
     return 0
 
 

@@ -74,3 +74,54 @@ def test_built_wconv_matches_its_schedule(toolchain):
     r = _check(lib, obj)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "16 wconv3_kernel instantiations match" in r.stdout
+
+
+def _sffn_listing():
+    sys.path.insert(0, os.path.join(REPO, "scripts"))
+    import check_xconv_vmcnt as c
+    obj = os.path.join(REPO, "build/hip/sffn.o")
+    if not os.path.exists(obj):
+        pytest.skip("sffn.o not built (make hip)")
+    return c.disassemble(obj)
+
+
+def _check_listing(tmp_path, text):
+    s = tmp_path / "sffn.s"
+    s.write_text(text)
+    return _check(os.path.join(REPO, "dcvc_amd/lib/libdcvc_hip.so"), str(s))
+
+
+def test_built_sffn_waits_for_each_slice(toolchain, tmp_path):
+    """sffn.hip's streamed kernels (C = 128: slices through four LDS buffers,
+    exact vmcnt waits): on every path to each barrier, the DMA the barrier
+    waits for has at least vmcnt(N) younger vector-memory instructions."""
+    r = _check_listing(tmp_path, _sffn_listing())
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "3 streamed sffn_kernel instantiations wait for each slice's DMA" in r.stdout
+
+
+def test_sffn_check_catches_a_lax_wait(toolchain, tmp_path):
+    """B_1 / B_2 of sffn_kernel<128, 4, 1, 4> wait vmcnt(NDW + PFN) = 16; 17
+    would let the slice's last DMA instruction still be in flight."""
+    text = _sffn_listing().replace("s_waitcnt vmcnt(16) lgkmcnt(0)", "s_waitcnt vmcnt(17) lgkmcnt(0)")
+    r = _check_listing(tmp_path, text)
+    assert r.returncode == 1, r.stdout + r.stderr
+    assert "sffn_kernel<128,4,1,4>" in r.stderr and "vmcnt(17)" in r.stderr, r.stderr
+
+
+def test_sffn_check_catches_a_hoisted_prefetch(toolchain, tmp_path):
+    """The next tile's input prefetch moved above B_0's slice DMA (what hipcc
+    could do: the two are independent): B_2's vmcnt(NDW + PFN) then no longer
+    covers slice 2's DMA, and the check says so."""
+    lines = _sffn_listing().splitlines()
+    start = next(i for i, ln in enumerate(lines) if "sffn_kernelILi128ELi4ELi1ELi4E" in ln and ln.endswith(">:"))
+    b0 = next(i for i in range(start, len(lines)) if "s_barrier" in lines[i])
+    b1 = next(i for i in range(b0 + 1, len(lines)) if "s_barrier" in lines[i])
+    loads = [i for i in range(b0 + 1, b1) if "buffer_load" in lines[i] and " lds" not in lines[i].split("//")[0]]
+    assert len(loads) == 8
+    moved = [lines[i] for i in loads]
+    rest = [ln for i, ln in enumerate(lines) if i not in set(loads)]
+    text = "\n".join(rest[:b0 + 1] + moved + rest[b0 + 1:])
+    r = _check_listing(tmp_path, text)
+    assert r.returncode == 1, r.stdout + r.stderr
+    assert "sffn_kernel<128,4,1,4>: barrier at" in r.stderr and "vmcnt(16), but only 8" in r.stderr, r.stderr
