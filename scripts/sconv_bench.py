@@ -37,11 +37,12 @@ def main():
         if name != "arm":   # (a label only: which library of an A/B run)
             K.set_option(name, int(val))
     for sh in a.shapes.split(","):
-        m = re.fullmatch(r"(\d+)x(\d+)@(\d+)x(\d+)(?:k(\d))?(?:s(\d))?(r?)(u?)(g?)", sh)
+        m = re.fullmatch(r"(\d+)x(\d+)@(\d+)x(\d+)(?:k(\d))?(?:s(\d))?(r{0,2})(u?)(g?)", sh)
         cin, cout, H, W = (int(m.group(i)) for i in range(1, 5))
         k = int(m.group(5) or 3)
         s = int(m.group(6) or 1)
-        res = m.group(7) == "r"
+        res = len(m.group(7)) >= 1
+        res2 = len(m.group(7)) == 2
         shuf = m.group(8) == "u"
         gate = m.group(9) == "g"
         gk = dict(in_op=K.IN_GATE, in_slope=0.1) if gate else {}
@@ -49,6 +50,8 @@ def main():
         x = K.from_nchw(torch.randn(1, 2 * cin if gate else cin, H, W, device=dev), K.F32)
         Ho, Wo = cw.out_hw(H, W)
         r = K.from_nchw(torch.randn(1, cout, Ho, Wo, device=dev), K.F32) if res else None
+        if res2:
+            gk["res2"] = K.from_nchw(torch.randn(1, cout, Ho, Wo, device=dev), K.F32)
         y = K.empty(Ho * 2, Wo * 2, cout // 4, K.F32, dev) if shuf else K.empty(Ho, Wo, cout, K.F32, dev)
         for _ in range(3):
             K.conv(cw, x, y, act=K.ACT_LRELU, slope=0.1, res=r, shuffle=shuf, **gk)
@@ -59,7 +62,7 @@ def main():
         e1.record()
         torch.cuda.synchronize()
         us = e0.elapsed_time(e1) * 1e3 / a.reps
-        nb = 4 * (H * W * cin * (2 if gate else 1) + Ho * Wo * cout * (2 if res else 1)) + cw.w.numel() * 2
+        nb = 4 * (H * W * cin * (2 if gate else 1) + Ho * Wo * cout * (1 + res + res2)) + cw.w.numel() * 2
         fl = 2.0 * Ho * Wo * cin * cout * k * k
         print(json.dumps({"shape": sh, "opt": a.opt, "kernel": K.lib().dcvc_last_kernel().decode(), "us": round(us, 2),
                           "gbs": round(nb / us / 1e3, 1), "tflops": round(fl / us / 1e6, 1),
